@@ -1,0 +1,113 @@
+/*
+ * p1hip.h -- C ABI of libp1hip.so, the MI355X (gfx950) drop-in for the
+ * bitcoin miner's nonce scan.
+ *
+ * Reference seam (paths relative to /root/reference, SRC = src/github.com/cmu440):
+ *   SRC/bitcoin/miner/miner.go:56-63   the loop this library replaces:
+ *       var min, minIndex uint64 = math.MaxUint64, 0
+ *       for i := req.Lower; i <= req.Upper; i++ {
+ *           res := bitcoin.Hash(req.Data, i)
+ *           if res < min { min = res; minIndex = i }
+ *       }
+ *   SRC/bitcoin/hash.go:13-17          bitcoin.Hash(msg, nonce) =
+ *       BigEndian.Uint64(SHA-256(fmt.Sprintf("%s %d", msg, nonce))[0:8])
+ *   SRC/bitcoin/message.go:18-44       Request{Data, Lower, Upper} in,
+ *                                      Result{Hash, Nonce} out.
+ * The reference has no FFI of its own; these are the entry points a cgo
+ * bridge in the miner binds (INTEGRATION.md shows the binding).
+ *
+ * Plain C: no HIP/torch types, caller-owned buffers, no allocation crosses
+ * the boundary.  `msg` is only borrowed for the duration of a call (cgo's
+ * pointer-passing rule).  All calls are synchronous and serialised
+ * internally; every call may be made from any host thread.
+ *
+ * Return codes: 0 ok; negative values are errors (details in
+ * p1hip_last_error(), a per-thread string).
+ */
+#ifndef P1HIP_H
+#define P1HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define P1HIP_OK 0
+#define P1HIP_ERR_NO_DEVICE (-1) /* no gfx950 device visible / bad ordinal      */
+#define P1HIP_ERR_HIP (-2)       /* HIP runtime error                           */
+#define P1HIP_ERR_RCCL (-3)      /* RCCL error (multi-device all-gather)        */
+#define P1HIP_ERR_ARGS (-4)      /* msg==NULL with msg_len>0, msg_len too large */
+
+/* Longest message accepted (bytes).  Keeps the SHA-256 bit length in one
+ * 32-bit word; the reference's LSP frames cap Data at ~1.3 KB anyway
+ * (SRC/lsp/common.go:7, 2000-byte receive buffers). */
+#define P1HIP_MAX_MSG_LEN ((size_t)1 << 28)
+
+/* Open `want_devices` devices (<= 0: every visible device), create one HIP
+ * stream per device and, when more than one device is used, one RCCL
+ * communicator per device (ncclCommInitAll).  Idempotent: a second call with
+ * the same count is a no-op; a different count re-initialises. */
+int p1hip_init(int want_devices, int *got_devices);
+
+/* Same, but with an explicit list of device ordinals (e.g. {LOCAL_RANK} for
+ * a one-process-per-GPU miner). */
+int p1hip_init_devices(const int *ordinals, int n);
+
+/* The drop-in for miner.go:56-63.  Scans [lower, upper] INCLUSIVE and
+ * returns the minimum bitcoin.Hash(msg, i) and its nonce; ties go to the
+ * lowest nonce (strict '<' at miner.go:59).  lower > upper returns
+ * (UINT64_MAX, 0) with rc 0, exactly like the reference loop.  If every hash
+ * in the range equals UINT64_MAX the nonce is 0 (identity of miner.go:56).
+ * Documented divergence: upper == UINT64_MAX is scanned inclusively and the
+ * call returns; the Go loop wraps (i++) and never terminates.
+ * With several devices the range is split contiguously across them and the
+ * 16-byte per-device partials are combined by an RCCL all-gather + host min.
+ * Lazily calls p1hip_init(0, NULL) if nothing is initialised. */
+int p1hip_scan(const uint8_t *msg, size_t msg_len, uint64_t lower, uint64_t upper,
+               uint64_t *out_hash, uint64_t *out_nonce);
+
+/* bitcoin.Hash(msg, nonce) (hash.go:13-17), computed on the GPU as the
+ * one-nonce scan [nonce, nonce]. */
+int p1hip_hash(const uint8_t *msg, size_t msg_len, uint64_t nonce, uint64_t *out_hash);
+
+/* Test hook for the device-side argmin: reduces n crafted (hash, nonce)
+ * pairs with the scan's own wave/LDS/grid reduction kernels and applies the
+ * same result rules as p1hip_scan (lexicographic (hash, nonce) minimum,
+ * nonce 0 when the minimum hash is UINT64_MAX, (UINT64_MAX, 0) when n == 0). */
+int p1hip_reduce_pairs(const uint64_t *hashes, const uint64_t *nonces, size_t n,
+                       uint64_t *out_hash, uint64_t *out_nonce);
+
+/* Kernel-level accounting for the dominant (fast scan) kernel. */
+typedef struct {
+  uint64_t scans;           /* p1hip_scan calls since reset                       */
+  uint64_t fast_launches;   /* launches of the fast scan kernel                   */
+  uint64_t fast_nonces;     /* nonces hashed by those launches                    */
+  uint64_t fast_alg_ops;    /* algorithmic int32 ops: 1384 * B_tail per nonce     */
+  double fast_kernel_ms;    /* sum of HIP-event durations of those launches
+                               (only while profiling is on, else 0)               */
+  uint64_t generic_launches;/* launches of the generic (edge) kernel              */
+  uint64_t generic_nonces;  /* nonces hashed by the generic kernel                */
+  double scan_wall_ms;      /* host wall time inside p1hip_scan                   */
+} p1hip_stats_t;
+
+/* Record HIP events (on the library's own stream) around every fast-kernel
+ * launch.  Off by default: the events cost a little host time per launch. */
+int p1hip_set_profiling(int on);
+int p1hip_get_stats(p1hip_stats_t *out);
+void p1hip_reset_stats(void);
+
+/* Number of devices currently in use (0 before init). */
+int p1hip_device_count(void);
+
+const char *p1hip_last_error(void);
+const char *p1hip_version(void);
+
+/* Release streams, buffers and communicators.  Safe to call twice. */
+void p1hip_shutdown(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* P1HIP_H */

@@ -1,0 +1,26 @@
+"""p1_amd -- MI355X (gfx950) drop-in for the bitcoin miner's nonce scan.
+
+The product is the C-ABI library ``p1_amd/libp1hip.so`` (include/p1hip.h).
+This package is thin Python plumbing over it (ctypes), used by bench.py and
+the tests.  There is no CPU fallback: every call goes to the HIP kernels and
+raises if the library or a gfx950 device is missing.
+
+Reference seam: /root/reference/src/github.com/cmu440/bitcoin/miner/miner.go:56-63.
+"""
+from ._lib import (  # noqa: F401
+    P1HipError,
+    lib_path,
+    load,
+    init,
+    init_devices,
+    scan,
+    hash,
+    reduce_pairs,
+    set_profiling,
+    get_stats,
+    reset_stats,
+    device_count,
+    shutdown,
+    version,
+)
+from .sharding import shard_range, combine_keys  # noqa: F401

@@ -1,0 +1,148 @@
+"""ctypes binding of libp1hip.so (declarations: include/p1hip.h).
+
+Fails loudly: a missing library, a missing symbol or a non-zero return code
+raises P1HipError.  Nothing here computes a hash on the CPU.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+U64 = ctypes.c_uint64
+
+
+class P1HipError(RuntimeError):
+    def __init__(self, rc, msg):
+        super().__init__(f"p1hip rc={rc}: {msg}")
+        self.rc = rc
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("scans", U64),
+        ("fast_launches", U64),
+        ("fast_nonces", U64),
+        ("fast_alg_ops", U64),
+        ("fast_kernel_ms", ctypes.c_double),
+        ("generic_launches", U64),
+        ("generic_nonces", U64),
+        ("scan_wall_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def lib_path():
+    return os.path.join(_HERE, "libp1hip.so")
+
+
+# (name, restype, argtypes) for every entry point of include/p1hip.h
+SIGNATURES = [
+    ("p1hip_init", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    ("p1hip_init_devices", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ("p1hip_scan", ctypes.c_int,
+     [ctypes.c_char_p, ctypes.c_size_t, U64, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+    ("p1hip_hash", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, U64, ctypes.POINTER(U64)]),
+    ("p1hip_reduce_pairs", ctypes.c_int,
+     [ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.c_size_t, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+    ("p1hip_set_profiling", ctypes.c_int, [ctypes.c_int]),
+    ("p1hip_get_stats", ctypes.c_int, [ctypes.POINTER(Stats)]),
+    ("p1hip_reset_stats", None, []),
+    ("p1hip_device_count", ctypes.c_int, []),
+    ("p1hip_last_error", ctypes.c_char_p, []),
+    ("p1hip_version", ctypes.c_char_p, []),
+    ("p1hip_shutdown", None, []),
+]
+
+
+def load(path=None):
+    """Load libp1hip.so (once).  Raises if it is missing or incomplete."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or lib_path()
+    if not os.path.exists(p):
+        raise P1HipError(-100, f"{p} not built (run `make` or __graft_entry__.build())")
+    lib = ctypes.CDLL(p)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)  # AttributeError if the export is missing
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise P1HipError(rc, load().p1hip_last_error().decode(errors="replace"))
+
+
+def _bytes(msg):
+    if isinstance(msg, str):
+        return msg.encode("utf-8")  # Go strings are UTF-8 bytes after the JSON round trip
+    return bytes(msg)
+
+
+def init(want_devices=0):
+    got = ctypes.c_int(0)
+    _check(load().p1hip_init(int(want_devices), ctypes.byref(got)))
+    return got.value
+
+
+def init_devices(ordinals):
+    arr = (ctypes.c_int * len(ordinals))(*ordinals)
+    _check(load().p1hip_init_devices(arr, len(ordinals)))
+
+
+def scan(msg, lower, upper):
+    """miner.go:56-63 on the GPU: (min hash, its nonce) over [lower, upper]."""
+    m = _bytes(msg)
+    h, n = U64(), U64()
+    _check(load().p1hip_scan(m, len(m), int(lower), int(upper), ctypes.byref(h), ctypes.byref(n)))
+    return h.value, n.value
+
+
+def hash(msg, nonce):  # noqa: A001 - mirrors bitcoin.Hash
+    m = _bytes(msg)
+    h = U64()
+    _check(load().p1hip_hash(m, len(m), int(nonce), ctypes.byref(h)))
+    return h.value
+
+
+def reduce_pairs(hashes, nonces):
+    n = len(hashes)
+    assert n == len(nonces)
+    ha = (U64 * max(n, 1))(*hashes)
+    na = (U64 * max(n, 1))(*nonces)
+    h, o = U64(), U64()
+    _check(load().p1hip_reduce_pairs(ha, na, n, ctypes.byref(h), ctypes.byref(o)))
+    return h.value, o.value
+
+
+def set_profiling(on):
+    _check(load().p1hip_set_profiling(1 if on else 0))
+
+
+def get_stats():
+    s = Stats()
+    _check(load().p1hip_get_stats(ctypes.byref(s)))
+    return s.as_dict()
+
+
+def reset_stats():
+    load().p1hip_reset_stats()
+
+
+def device_count():
+    return load().p1hip_device_count()
+
+
+def shutdown():
+    load().p1hip_shutdown()
+
+
+def version():
+    return load().p1hip_version().decode()

@@ -1,0 +1,509 @@
+// p1hip.hip -- libp1hip.so: gfx950 kernels, launch orchestration and the C ABI
+// declared in include/p1hip.h.
+//
+// Replaces the miner's scan loop /root/reference/src/github.com/cmu440/bitcoin/
+// miner/miner.go:56-63 (see include/p1hip.h for the exact contract).
+//
+// Device pipeline of one p1hip_scan on one device (one HIP stream):
+//   planner.hpp  -> list of launches (fast: one thread per 10^k nonces;
+//                   generic: one thread per nonce, for ragged edges)
+//   k_scan_fast<FV,NV,TRAIL> / k_scan_generic
+//                -> per-thread best (hash, nonce) -> wave argmin with DPP
+//                   (quad_perm, row_ror) + ds_swizzle + readlane -> LDS across
+//                   the 4 waves -> one 16-byte partial per workgroup
+//   k_reduce     -> one workgroup folds all partials into the device result
+// Several devices: contiguous shards, one host thread per device, RCCL
+// all-gather of the 16-byte results (ncclCommInitAll), host lexicographic min.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/p1hip.h"
+#include "planner.hpp"
+
+using namespace p1;
+
+// ----------------------------------------------------------------------------
+// Wave / workgroup argmin over Key = (hash, nonce), lexicographic.
+// ----------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+template <int CTRL>
+__device__ __forceinline__ Key key_dpp(const Key& k) {
+  Key o;
+  o.h = ((uint64_t)dpp<CTRL>((uint32_t)(k.h >> 32)) << 32) | dpp<CTRL>((uint32_t)k.h);
+  o.n = ((uint64_t)dpp<CTRL>((uint32_t)(k.n >> 32)) << 32) | dpp<CTRL>((uint32_t)k.n);
+  return o;
+}
+
+__device__ __forceinline__ uint32_t swz_xor16(uint32_t v) {
+  // ds_swizzle bit-mask mode: and 0x1f, or 0, xor 0x10 (within 32 lanes)
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
+}
+
+__device__ __forceinline__ Key key_min(const Key& a, const Key& b) { return key_lt(b, a) ? b : a; }
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// All 64 lanes must be active.  Returns the wave minimum (wave-uniform).
+__device__ __forceinline__ Key wave_min(Key k) {
+  k = key_min(k, key_dpp<0xB1>(k));   // quad_perm [1,0,3,2]  (xor 1)
+  k = key_min(k, key_dpp<0x4E>(k));   // quad_perm [2,3,0,1]  (xor 2)
+  k = key_min(k, key_dpp<0x124>(k));  // row_ror:4
+  k = key_min(k, key_dpp<0x128>(k));  // row_ror:8  -> every lane holds its row min
+  Key o;
+  o.h = ((uint64_t)swz_xor16((uint32_t)(k.h >> 32)) << 32) | swz_xor16((uint32_t)k.h);
+  o.n = ((uint64_t)swz_xor16((uint32_t)(k.n >> 32)) << 32) | swz_xor16((uint32_t)k.n);
+  k = key_min(k, o);                  // halves of 32 lanes
+  Key a, b;
+  a.h = readlane64(k.h, 0);  a.n = readlane64(k.n, 0);
+  b.h = readlane64(k.h, 32); b.n = readlane64(k.n, 32);
+  return key_min(a, b);
+}
+
+template <int NT>
+__device__ __forceinline__ void block_min_store(Key k, Key* out) {
+  __shared__ Key sk[NT / 64];
+  k = wave_min(k);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) sk[wid] = k;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Key b = sk[0];
+#pragma unroll
+    for (int w = 1; w < NT / 64; ++w) b = key_min(b, sk[w]);
+    *out = b;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Kernels
+// ----------------------------------------------------------------------------
+template <int FV, int NV, bool TRAIL>
+__global__ __launch_bounds__(kBlock) void k_scan_fast(const FastArgs A, Key* __restrict__ part) {
+  const Key k = fast_thread<FV, NV, TRAIL>(A, blockIdx.x * kBlock + threadIdx.x);
+  block_min_store<kBlock>(k, part + A.part_off + blockIdx.x);
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_generic(const GenArgs A, Key* __restrict__ part) {
+  const Key k = generic_thread(A, (uint64_t)blockIdx.x * kBlock + threadIdx.x);
+  block_min_store<kBlock>(k, part + A.part_off + blockIdx.x);
+}
+
+constexpr int kReduceThreads = 1024;
+
+__global__ __launch_bounds__(kReduceThreads) void k_reduce(const Key* __restrict__ part, uint32_t n,
+                                                           Key* __restrict__ out) {
+  Key b = {~0ull, ~0ull};
+  for (uint32_t i = threadIdx.x; i < n; i += kReduceThreads) b = key_min(b, part[i]);
+  block_min_store<kReduceThreads>(b, out);
+}
+
+// test hook: one crafted pair per thread -> per-workgroup partials
+__global__ __launch_bounds__(kBlock) void k_pairs(const uint64_t* __restrict__ hs, const uint64_t* __restrict__ ns,
+                                                  uint64_t n, Key* __restrict__ part) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  Key k = {~0ull, ~0ull};
+  if (i < n) { k.h = hs[i]; k.n = ns[i]; }
+  block_min_store<kBlock>(k, part + blockIdx.x);
+}
+
+typedef void (*FastKernel)(const FastArgs, Key*);
+
+static FastKernel fast_kernel(int fv, int nv, bool trail) {
+#define P1_CASE(FV, NV, TR) \
+  if (fv == FV && nv == NV && trail == TR) return &k_scan_fast<FV, NV, TR>;
+#include "fast_variants.inc"
+#undef P1_CASE
+  return nullptr;
+}
+
+// ----------------------------------------------------------------------------
+// Runtime state
+// ----------------------------------------------------------------------------
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int rc, const std::string& what) {
+  g_err = what;
+  return rc;
+}
+
+#define HIPCHK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return fail(P1HIP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+  } while (0)
+
+#define NCCLCHK(expr)                                                                       \
+  do {                                                                                      \
+    ncclResult_t r_ = (expr);                                                               \
+    if (r_ != ncclSuccess)                                                                  \
+      return fail(P1HIP_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_));      \
+  } while (0)
+
+struct Dev {
+  int ordinal = -1;
+  hipStream_t stream = nullptr;
+  Key* d_part = nullptr;
+  size_t part_cap = 0;
+  Key* d_res = nullptr;     // 1 Key
+  Key* d_gather = nullptr;  // ndev Keys (multi-device)
+  Key* h_res = nullptr;     // pinned, ndev Keys
+  ncclComm_t comm = nullptr;
+  std::vector<hipEvent_t> evs;  // profiling event pool (pairs)
+  // per-scan accounting filled by run_plan
+  uint64_t fast_launches = 0, fast_nonces = 0, fast_ops = 0, gen_launches = 0, gen_nonces = 0;
+  double fast_ms = 0.0;
+};
+
+struct Runtime {
+  std::mutex mu;
+  std::vector<Dev> devs;
+  bool profiling = false;
+  p1hip_stats_t stats{};
+};
+
+Runtime& rt() {
+  static Runtime r;
+  return r;
+}
+
+int dev_release(Dev& d) {
+  if (d.ordinal < 0) return 0;
+  (void)hipSetDevice(d.ordinal);
+  if (d.stream) (void)hipStreamSynchronize(d.stream);
+  for (hipEvent_t e : d.evs) (void)hipEventDestroy(e);
+  d.evs.clear();
+  if (d.comm) ncclCommDestroy(d.comm);
+  if (d.d_part) (void)hipFree(d.d_part);
+  if (d.d_res) (void)hipFree(d.d_res);
+  if (d.d_gather) (void)hipFree(d.d_gather);
+  if (d.h_res) (void)hipHostFree(d.h_res);
+  if (d.stream) (void)hipStreamDestroy(d.stream);
+  d = Dev();
+  return 0;
+}
+
+void shutdown_locked(Runtime& R) {
+  for (Dev& d : R.devs) dev_release(d);
+  R.devs.clear();
+}
+
+int init_locked(Runtime& R, const std::vector<int>& ords) {
+  if (!R.devs.empty()) {
+    bool same = R.devs.size() == ords.size();
+    for (size_t i = 0; same && i < ords.size(); ++i) same = R.devs[i].ordinal == ords[i];
+    if (same) return P1HIP_OK;
+    shutdown_locked(R);
+  }
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+    return fail(P1HIP_ERR_NO_DEVICE, "no HIP device visible");
+  for (int o : ords) {
+    if (o < 0 || o >= count) return fail(P1HIP_ERR_NO_DEVICE, "device ordinal out of range: " + std::to_string(o));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, o));
+    if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
+      return fail(P1HIP_ERR_NO_DEVICE, std::string("device is not gfx950: ") + prop.gcnArchName);
+  }
+  R.devs.resize(ords.size());
+  const int nd = (int)ords.size();
+  for (int i = 0; i < nd; ++i) {
+    Dev& d = R.devs[i];
+    d.ordinal = ords[i];
+    HIPCHK(hipSetDevice(d.ordinal));
+    HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&d.d_res, sizeof(Key)));
+    HIPCHK(hipMalloc(&d.d_gather, sizeof(Key) * nd));
+    HIPCHK(hipHostMalloc(&d.h_res, sizeof(Key) * nd, hipHostMallocDefault));
+  }
+  if (nd > 1) {
+    std::vector<ncclComm_t> comms(nd);
+    NCCLCHK(ncclCommInitAll(comms.data(), nd, ords.data()));
+    for (int i = 0; i < nd; ++i) R.devs[i].comm = comms[i];
+  }
+  return P1HIP_OK;
+}
+
+int ensure_init(Runtime& R) {
+  if (!R.devs.empty()) return P1HIP_OK;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+    return fail(P1HIP_ERR_NO_DEVICE, "no HIP device visible");
+  std::vector<int> ords;
+  for (int i = 0; i < count; ++i) ords.push_back(i);
+  return init_locked(R, ords);
+}
+
+// Run one device's share [lo, hi] (lo <= hi) and leave its Key in d.d_res.
+int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, bool profiling) {
+  HIPCHK(hipSetDevice(d.ordinal));
+  d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
+  d.fast_ms = 0.0;
+  Plan plan;
+  std::string err = make_plan(msg, len, lo, hi, plan);
+  if (!err.empty()) return fail(P1HIP_ERR_ARGS, "planner: " + err);
+  if (plan.total_blocks > d.part_cap) {
+    if (d.d_part) HIPCHK(hipFree(d.d_part));
+    d.d_part = nullptr;
+    size_t cap = 1;
+    while (cap < plan.total_blocks) cap <<= 1;
+    HIPCHK(hipMalloc(&d.d_part, cap * sizeof(Key)));
+    d.part_cap = cap;
+  }
+  size_t nev = 0;
+  for (const Launch& L : plan.launches) {
+    if (L.fast) {
+      FastKernel fn = fast_kernel(L.fv, L.nv, L.trail);
+      if (!fn) return fail(P1HIP_ERR_ARGS, "no fast kernel variant");
+      if (profiling) {
+        while (d.evs.size() < nev + 2) {
+          hipEvent_t e;
+          HIPCHK(hipEventCreate(&e));
+          d.evs.push_back(e);
+        }
+        HIPCHK(hipEventRecord(d.evs[nev], d.stream));
+      }
+      hipLaunchKernelGGL(fn, dim3(L.blocks), dim3(kBlock), 0, d.stream, L.fa, d.d_part);
+      HIPCHK(hipGetLastError());
+      if (profiling) {
+        HIPCHK(hipEventRecord(d.evs[nev + 1], d.stream));
+        nev += 2;
+      }
+      d.fast_launches++;
+      d.fast_nonces += L.nonces;
+      d.fast_ops += L.nonces * kAlgOpsPerCompression * (uint64_t)L.btail;
+    } else {
+      hipLaunchKernelGGL(k_scan_generic, dim3(L.blocks), dim3(kBlock), 0, d.stream, L.ga, d.d_part);
+      HIPCHK(hipGetLastError());
+      d.gen_launches++;
+      d.gen_nonces += L.nonces;
+    }
+  }
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, d.stream, d.d_part, plan.total_blocks,
+                     d.d_res);
+  HIPCHK(hipGetLastError());
+  if (profiling && nev) {
+    HIPCHK(hipEventSynchronize(d.evs[nev - 1]));
+    for (size_t i = 0; i < nev; i += 2) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, d.evs[i], d.evs[i + 1]));
+      d.fast_ms += ms;
+    }
+  }
+  return P1HIP_OK;
+}
+
+Key finish_key(Key k) {
+  if (k.h == ~0ull) k.n = 0;  // identity (MaxUint64, 0) of miner.go:56
+  return k;
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------
+// C ABI
+// ----------------------------------------------------------------------------
+extern "C" {
+
+int p1hip_init(int want_devices, int* got_devices) {
+  Runtime& R = rt();
+  std::lock_guard<std::mutex> g(R.mu);
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+    return fail(P1HIP_ERR_NO_DEVICE, "no HIP device visible");
+  int n = want_devices <= 0 ? count : want_devices;
+  if (n > count) return fail(P1HIP_ERR_NO_DEVICE, "asked for more devices than visible");
+  std::vector<int> ords;
+  for (int i = 0; i < n; ++i) ords.push_back(i);
+  int rc = init_locked(R, ords);
+  if (got_devices) *got_devices = rc == 0 ? (int)R.devs.size() : 0;
+  return rc;
+}
+
+int p1hip_init_devices(const int* ordinals, int n) {
+  if (!ordinals || n <= 0) return fail(P1HIP_ERR_ARGS, "empty device list");
+  Runtime& R = rt();
+  std::lock_guard<std::mutex> g(R.mu);
+  return init_locked(R, std::vector<int>(ordinals, ordinals + n));
+}
+
+int p1hip_device_count(void) {
+  Runtime& R = rt();
+  std::lock_guard<std::mutex> g(R.mu);
+  return (int)R.devs.size();
+}
+
+int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t upper, uint64_t* out_hash,
+               uint64_t* out_nonce) {
+  if (!out_hash || !out_nonce) return fail(P1HIP_ERR_ARGS, "null output pointer");
+  if (!msg && msg_len > 0) return fail(P1HIP_ERR_ARGS, "msg == NULL with msg_len > 0");
+  if (msg_len > P1HIP_MAX_MSG_LEN) return fail(P1HIP_ERR_ARGS, "msg_len exceeds P1HIP_MAX_MSG_LEN");
+  Runtime& R = rt();
+  std::lock_guard<std::mutex> g(R.mu);
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = ensure_init(R);
+  if (rc) return rc;
+  Key res = {~0ull, 0};
+  if (lower <= upper) {
+    const size_t nd = R.devs.size();
+    // contiguous shards: shard i = [lo_i, hi_i]
+    const uint64_t span = upper - lower;  // count - 1
+    std::vector<uint64_t> slo(nd), shi(nd);
+    std::vector<char> active(nd, 0);
+    {
+      const uint64_t per = span / nd, extra = span % nd;
+      uint64_t cur = lower;
+      for (size_t i = 0; i < nd; ++i) {
+        // sizes: per (+1 for the first `extra`), +1 on the last -> sum span+1
+        uint64_t cnt = per + (i < extra ? 1u : 0u) + (i + 1 == nd ? 1u : 0u);
+        if (cnt == 0) continue;
+        active[i] = 1;
+        slo[i] = cur;
+        shi[i] = cur + (cnt - 1);
+        cur += cnt;
+      }
+    }
+    std::vector<int> rcs(nd, 0);
+    std::vector<std::string> errs(nd);
+    auto work = [&](size_t i) {
+      Dev& d = R.devs[i];
+      int r = P1HIP_OK;
+      if (active[i]) {
+        r = run_range(d, msg, msg_len, slo[i], shi[i], R.profiling);
+      } else {
+        if (hipSetDevice(d.ordinal) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipSetDevice");
+        const Key idk = {~0ull, ~0ull};
+        if (!r && hipMemcpyAsync(d.d_res, &idk, sizeof idk, hipMemcpyHostToDevice, d.stream) != hipSuccess)
+          r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(identity)");
+      }
+      if (!r && nd > 1) {
+        ncclResult_t nr = ncclAllGather(d.d_res, d.d_gather, 2, ncclUint64, d.comm, d.stream);
+        if (nr != ncclSuccess) r = fail(P1HIP_ERR_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
+      }
+      if (!r && i == 0) {
+        const Key* src = nd > 1 ? d.d_gather : d.d_res;
+        if (hipMemcpyAsync(d.h_res, src, sizeof(Key) * nd, hipMemcpyDeviceToHost, d.stream) != hipSuccess)
+          r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(result)");
+      }
+      if (!r && hipStreamSynchronize(d.stream) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipStreamSynchronize");
+      rcs[i] = r;
+      if (r) errs[i] = g_err;
+    };
+    if (nd == 1) {
+      work(0);
+    } else {
+      std::vector<std::thread> th;
+      for (size_t i = 0; i < nd; ++i) th.emplace_back(work, i);
+      for (auto& t : th) t.join();
+    }
+    for (size_t i = 0; i < nd; ++i)
+      if (rcs[i]) return fail(rcs[i], "device " + std::to_string(R.devs[i].ordinal) + ": " + errs[i]);
+    Key b = {~0ull, ~0ull};
+    for (size_t i = 0; i < nd; ++i) b = key_lt(R.devs[0].h_res[i], b) ? R.devs[0].h_res[i] : b;
+    res = finish_key(b);
+    for (Dev& d : R.devs) {
+      R.stats.fast_launches += d.fast_launches;
+      R.stats.fast_nonces += d.fast_nonces;
+      R.stats.fast_alg_ops += d.fast_ops;
+      R.stats.fast_kernel_ms += d.fast_ms;
+      R.stats.generic_launches += d.gen_launches;
+      R.stats.generic_nonces += d.gen_nonces;
+    }
+  }
+  R.stats.scans++;
+  R.stats.scan_wall_ms +=
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out_hash = res.h;
+  *out_nonce = res.n;
+  return P1HIP_OK;
+}
+
+int p1hip_hash(const uint8_t* msg, size_t msg_len, uint64_t nonce, uint64_t* out_hash) {
+  uint64_t n = 0;
+  return p1hip_scan(msg, msg_len, nonce, nonce, out_hash, &n);
+}
+
+int p1hip_reduce_pairs(const uint64_t* hashes, const uint64_t* nonces, size_t n, uint64_t* out_hash,
+                       uint64_t* out_nonce) {
+  if (!out_hash || !out_nonce || (n && (!hashes || !nonces))) return fail(P1HIP_ERR_ARGS, "null pointer");
+  Runtime& R = rt();
+  std::lock_guard<std::mutex> g(R.mu);
+  int rc = ensure_init(R);
+  if (rc) return rc;
+  Dev& d = R.devs[0];
+  HIPCHK(hipSetDevice(d.ordinal));
+  Key res = {~0ull, ~0ull};
+  if (n) {
+    uint64_t *dh = nullptr, *dn = nullptr;
+    Key* dp = nullptr;
+    const uint32_t blocks = (uint32_t)((n + kBlock - 1) / kBlock);
+    HIPCHK(hipMalloc(&dh, n * 8));
+    HIPCHK(hipMalloc(&dn, n * 8));
+    HIPCHK(hipMalloc(&dp, (size_t)blocks * sizeof(Key)));
+    HIPCHK(hipMemcpyAsync(dh, hashes, n * 8, hipMemcpyHostToDevice, d.stream));
+    HIPCHK(hipMemcpyAsync(dn, nonces, n * 8, hipMemcpyHostToDevice, d.stream));
+    hipLaunchKernelGGL(k_pairs, dim3(blocks), dim3(kBlock), 0, d.stream, dh, dn, (uint64_t)n, dp);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, d.stream, dp, blocks, d.d_res);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(d.h_res, d.d_res, sizeof(Key), hipMemcpyDeviceToHost, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    res = d.h_res[0];
+    (void)hipFree(dh);
+    (void)hipFree(dn);
+    (void)hipFree(dp);
+  }
+  res = finish_key(res);
+  *out_hash = res.h;
+  *out_nonce = res.n;
+  return P1HIP_OK;
+}
+
+int p1hip_set_profiling(int on) {
+  Runtime& R = rt();
+  std::lock_guard<std::mutex> g(R.mu);
+  R.profiling = on != 0;
+  return P1HIP_OK;
+}
+
+int p1hip_get_stats(p1hip_stats_t* out) {
+  if (!out) return fail(P1HIP_ERR_ARGS, "null stats pointer");
+  Runtime& R = rt();
+  std::lock_guard<std::mutex> g(R.mu);
+  *out = R.stats;
+  return P1HIP_OK;
+}
+
+void p1hip_reset_stats(void) {
+  Runtime& R = rt();
+  std::lock_guard<std::mutex> g(R.mu);
+  R.stats = p1hip_stats_t{};
+}
+
+const char* p1hip_last_error(void) { return g_err.c_str(); }
+
+const char* p1hip_version(void) { return "p1hip 0.1 gfx950"; }
+
+void p1hip_shutdown(void) {
+  Runtime& R = rt();
+  std::lock_guard<std::mutex> g(R.mu);
+  shutdown_locked(R);
+}
+
+}  // extern "C"

@@ -1,0 +1,243 @@
+// scan_core.hpp -- per-thread work of the nonce-scan kernels.
+//
+// Reference loop: /root/reference/src/github.com/cmu440/bitcoin/miner/miner.go:56-63
+// (min over i in [Lower, Upper] of bitcoin.Hash(Data, i), strict '<').
+// bitcoin.Hash:   /root/reference/src/github.com/cmu440/bitcoin/hash.go:13-17
+// (SHA-256 of  msg ' ' decimal(nonce), first 8 digest bytes big-endian).
+//
+// Data layout (all in registers / kernel arguments; no HBM traffic besides
+// one 16-byte partial per workgroup):
+//   * "prefix" = msg || ' ' (L+1 bytes).  Its floor((L+1)/64) full blocks are
+//     compressed once on the host into `mid` (the midstate).
+//   * "tail" = the remaining r = (L+1) mod 64 prefix bytes, the d decimal
+//     digits of the nonce, 0x80, zeros and the 64-bit bit length: one or two
+//     64-byte blocks (B_tail), kept as 32 big-endian words `tmpl[32]`.
+//   * A decade segment (every nonce with the same digit count d) is split as
+//     nonce = hi * 10^k + lo.  One GPU thread owns one `hi` and loops over the
+//     10^k values of `lo` (k = 3 normally).  Its hi digits are formatted once
+//     per thread; the lo digits are ASCII-incremented in one or two message
+//     words (`FV`, `FV+1`) inside the loop, so per nonce only the rounds from
+//     word FV on and the schedule words that depend on them are recomputed.
+//   * Tail blocks before the "variable" block are thread-constant and are
+//     compressed once per thread (PRE); a tail block after it (TRAIL) has a
+//     constant message, so its K[t]+W[t] are host-precomputed (kw2).
+//
+// These functions are __host__ __device__ only so tools/p1emu can replay the
+// identical per-thread logic on the host in layout tests.
+#pragma once
+#include "sha256_dev.hpp"
+
+namespace p1 {
+
+constexpr int kBlock = 256;  // threads per workgroup (4 waves of 64)
+
+struct Key {
+  uint64_t h;  // bitcoin.Hash value
+  uint64_t n;  // nonce
+};
+
+P1_HD bool key_lt(const Key& a, const Key& b) {
+  return a.h < b.h || (a.h == b.h && a.n < b.n);
+}
+
+// Arguments of the fast kernel (one decade segment, aligned 10^k blocks).
+struct FastArgs {
+  uint32_t mid[8];    // chaining value entering the tail
+  uint32_t tmpl[32];  // tail words; '0' at lo-digit bytes, 0 at hi-digit bytes
+  uint32_t kw2[64];   // TRAIL: K[t] + W[t] of the constant last block
+  uint64_t hi_first;  // hi of thread 0
+  uint32_t nthreads;  // number of hi values in this launch
+  uint32_t dh;        // hi digit count (= d - k)
+  uint32_t p_last;    // tail byte index of the last hi digit
+  uint32_t pre;       // 1: variable block is tail block 1, block 0 per-thread
+  uint32_t kpow;      // 10^k
+  uint32_t n1, n2;    // trip counts of the tens / hundreds digit loops (1 or 10)
+  uint32_t du[2];     // units-digit increment of words FV, FV+1
+  uint32_t dt[2];     // tens carry:     (tens delta) - 10 * du
+  uint32_t dhd[2];    // hundreds carry: (hundreds delta) - 10 * (tens delta)
+  uint32_t part_off;  // first partial slot of this launch
+};
+
+// Arguments of the generic kernel (one nonce per thread, any layout).
+struct GenArgs {
+  uint32_t mid[8];
+  uint32_t tmpl[32];  // 0 at every digit byte
+  uint64_t lo;        // first nonce
+  uint64_t count;     // nonces in this launch
+  uint32_t d;         // digit count
+  uint32_t p_last;    // tail byte index of the last digit
+  uint32_t nb;        // tail blocks (1 or 2)
+  uint32_t part_off;
+};
+
+// Write the `ndig` low decimal digits of x (leading zeros kept) as ASCII so
+// that the last digit lands on tail byte p_last, OR-ing into tmpl words.
+// The digits are built right-aligned in a 24-byte window at compile-time
+// positions, funnel-shifted to the uniform byte phase and merged at a
+// uniform word offset, so no register array is ever indexed at run time.
+P1_HD void place_digits(const uint32_t* tmpl, uint64_t x, uint32_t ndig, uint32_t p_last,
+                        uint32_t T[32]) {
+  uint32_t G[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 20; ++j) {
+    const uint64_t q = x / 10u;
+    const uint32_t dig = (uint32_t)(x - q * 10u);
+    x = q;
+    const uint32_t c = ((uint32_t)j < ndig) ? (dig + 0x30u) : 0u;
+    G[5 - j / 4] |= c << (8 * (j % 4));
+  }
+  // window byte 23 <-> tail byte p_last; window byte 0 <-> tail byte p_last-23
+  const uint32_t start = p_last + 9u;  // (p_last - 23) + 32, never negative
+  const uint32_t sb = start & 3u;
+  const int wb = (int)(start >> 2) - 8;  // tail word of H[0]
+  uint32_t H[7];
+#pragma unroll
+  for (int m = 0; m < 7; ++m) {
+    const uint32_t hi = (m == 0) ? 0u : G[m - 1];
+    const uint32_t lo = (m == 6) ? 0u : G[m];
+    H[m] = funnel(hi, lo, 8u * sb);
+  }
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int idx = i - wb;
+    uint32_t v = 0;
+#pragma unroll
+    for (int m = 0; m < 7; ++m) v = (idx == m) ? H[m] : v;
+    T[i] = tmpl[i] | v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fast path: thread `tid` scans nonces hi*10^k + [0, 10^k).
+// FV = first message word of the variable block holding lo digits,
+// NV = number of such words (1 or 2), TRAIL = a constant block follows.
+// Words of the variable block:  i <  FV       thread-constant
+//                               FV..FV+NV-1   per nonce
+//                               FV+NV         uniform (pad byte or 0)
+//                               > FV+NV       0, except W15 = bit length
+//                                             when !TRAIL (host-checked)
+// ---------------------------------------------------------------------------
+template <int FV, int NV, bool TRAIL>
+P1_HD uint64_t fast_tail_hash(const State& s_fv, const uint32_t cv[8], const uint32_t Wt[16],
+                              uint32_t wv0, uint32_t wv1, uint32_t wu, uint32_t wlen,
+                              const uint32_t* kw2) {
+  uint32_t w[64];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i < FV) w[i] = Wt[i];
+    else if (i == FV) w[i] = wv0;
+    else if (NV == 2 && i == FV + 1) w[i] = wv1;
+    else if (i == FV + NV) w[i] = wu;
+    else if (!TRAIL && i == 15) w[i] = wlen;
+    else w[i] = 0u;
+  }
+#pragma unroll
+  for (int t = 16; t < 64; ++t) w[t] = sched(w, t);
+  State s = s_fv;
+#pragma unroll
+  for (int t = FV; t < 64; ++t) sha_round(s, k256(t) + w[t]);
+  if constexpr (!TRAIL) {
+    return ((uint64_t)(cv[0] + s.v[0]) << 32) | (uint64_t)(cv[1] + s.v[1]);
+  } else {
+    uint32_t cv2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cv2[i] = cv[i] + s.v[i];
+    State s2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s2.v[i] = cv2[i];
+#pragma unroll
+    for (int t = 0; t < 64; ++t) sha_round(s2, kw2[t]);
+    return ((uint64_t)(cv2[0] + s2.v[0]) << 32) | (uint64_t)(cv2[1] + s2.v[1]);
+  }
+}
+
+template <int FV, int NV, bool TRAIL>
+P1_HD Key fast_thread(const FastArgs& A, uint32_t tid) {
+  const bool valid = tid < A.nthreads;
+  const uint64_t hi = A.hi_first + (valid ? tid : 0u);
+
+  uint32_t T[32];
+  place_digits(A.tmpl, hi, A.dh, A.p_last, T);
+
+  uint32_t cv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cv[i] = A.mid[i];
+  const bool pre = A.pre != 0;
+  if (pre) {  // tail block 0 holds only prefix bytes and hi digits
+    uint32_t w[64];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = T[i];
+    compress_full(cv, w);
+  }
+  // variable block = tail block `pre`; a mask blend (not a select) keeps the
+  // compiler from lowering this to a runtime-indexed scratch array
+  const uint32_t pm = 0u - (uint32_t)pre;
+  uint32_t Wt[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) Wt[i] = (T[i] & ~pm) | (T[16 + i] & pm);
+  const uint32_t wu = (FV + NV < 16) ? (pre ? A.tmpl[16 + FV + NV] : A.tmpl[FV + NV]) : 0u;
+  const uint32_t wlen = pre ? A.tmpl[31] : A.tmpl[15];
+
+  // rounds 0..FV-1 see only thread-constant words
+  State s_fv;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s_fv.v[i] = cv[i];
+#pragma unroll
+  for (int t = 0; t < FV; ++t) sha_round(s_fv, k256(t) + Wt[t]);
+
+  uint32_t wv0 = Wt[FV];
+  uint32_t wv1 = (NV == 2) ? Wt[FV + 1] : 0u;
+  uint64_t best = ~0ull;
+  uint32_t bestc = 0;
+  uint32_t c = 0;
+  for (uint32_t c2 = 0; c2 < A.n2; ++c2) {
+    for (uint32_t c1 = 0; c1 < A.n1; ++c1) {
+      for (uint32_t c0 = 0; c0 < 10u; ++c0) {
+        const uint64_t h = fast_tail_hash<FV, NV, TRAIL>(s_fv, cv, Wt, wv0, wv1, wu, wlen, A.kw2);
+        const bool lt = h < best;  // strict '<': first minimum wins (miner.go:59)
+        best = lt ? h : best;
+        bestc = lt ? c : bestc;
+        ++c;
+        wv0 += A.du[0];
+        if (NV == 2) wv1 += A.du[1];
+      }
+      wv0 += A.dt[0];
+      if (NV == 2) wv1 += A.dt[1];
+    }
+    wv0 += A.dhd[0];
+    if (NV == 2) wv1 += A.dhd[1];
+  }
+  Key k;
+  k.h = valid ? best : ~0ull;
+  k.n = valid ? hi * (uint64_t)A.kpow + bestc : ~0ull;
+  return k;
+}
+
+// ---------------------------------------------------------------------------
+// Generic path: one nonce per thread, any tail layout (edges of a range,
+// decades with d <= k, and layouts where the lo digits straddle blocks).
+// ---------------------------------------------------------------------------
+P1_HD Key generic_thread(const GenArgs& A, uint64_t gid) {
+  const bool valid = gid < A.count;
+  const uint64_t n = A.lo + (valid ? gid : 0u);
+  uint32_t T[32];
+  place_digits(A.tmpl, n, A.d, A.p_last, T);
+  uint32_t cv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cv[i] = A.mid[i];
+  uint32_t w[64];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w[i] = T[i];
+  compress_full(cv, w);
+  if (A.nb == 2) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = T[16 + i];
+    compress_full(cv, w);
+  }
+  Key k;
+  k.h = valid ? (((uint64_t)cv[0] << 32) | cv[1]) : ~0ull;
+  k.n = valid ? n : ~0ull;
+  return k;
+}
+
+}  // namespace p1

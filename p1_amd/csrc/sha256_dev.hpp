@@ -1,0 +1,140 @@
+// sha256_dev.hpp -- gfx950 SHA-256 building blocks for the nonce scan.
+//
+// FIPS 180-4 section 6.2.2 compression, written for CDNA4's 32-bit VALU:
+//   rotr      -> v_alignbit_b32 (funnel shift of x:x)
+//   Ch / Maj  -> one v_bitop3_b32 each (truth tables 0xCA / 0xE8)
+//   xor3      -> one v_bitop3_b32 (0x96) for the three rotations of S0/S1/s0/s1
+//   T1, a'    -> v_add3_u32 (selected by the compiler from the '+' chains)
+// gfx950 has no bitop3 builtin, so the three-input logic ops are one-line
+// non-volatile inline asm without a memory clobber (the compiler may still
+// hoist or CSE them).  Every helper folds to a constant when its inputs are
+// compile-time constants (`__builtin_constant_p`, resolved after
+// unrolling/inlining), so zero words of the message schedule cost nothing.
+//
+// The helpers are __host__ __device__ only so that tools/p1emu can run the
+// exact per-thread scan logic on the host for layout tests; the host branch
+// is plain C and is never linked into libp1hip.so's scan path.
+//
+// Reference semantics: bitcoin.Hash = SHA-256 of "msg nonce"
+// (/root/reference/src/github.com/cmu440/bitcoin/hash.go:13-17); SHA-256
+// itself is Go stdlib crypto/sha256 (not in the reference tree).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define P1_HD __host__ __device__ __forceinline__
+
+namespace p1 {
+
+P1_HD constexpr uint32_t k256(int t) {
+  constexpr uint32_t k[64] = {
+      0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+      0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+      0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+      0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+      0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+      0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+      0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+      0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+  return k[t];
+}
+
+P1_HD constexpr uint32_t iv256(int i) {
+  constexpr uint32_t v[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                             0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  return v[i];
+}
+
+#define P1_CONST3(a, b, c) (__builtin_constant_p(a) && __builtin_constant_p(b) && __builtin_constant_p(c))
+
+P1_HD uint32_t rotr(uint32_t x, uint32_t n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (!__builtin_constant_p(x)) return __builtin_amdgcn_alignbit(x, x, n);
+#endif
+  return (x >> n) | (x << ((32u - n) & 31u));
+}
+
+// Funnel shift: low 32 bits of (hi:lo) >> s, s in [0, 31].
+P1_HD uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(hi, lo, s);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> s);
+#endif
+}
+
+P1_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (!P1_CONST3(a, b, c)) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+  }
+#endif
+  return a ^ b ^ c;
+}
+
+// Ch(e,f,g) = (e & f) ^ (~e & g)
+P1_HD uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (!P1_CONST3(e, f, g)) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(e), "v"(f), "v"(g));
+    return r;
+  }
+#endif
+  return (e & f) ^ (~e & g);
+}
+
+// Maj(a,b,c) = (a & b) ^ (a & c) ^ (b & c)
+P1_HD uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (!P1_CONST3(a, b, c)) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+  }
+#endif
+  return (a & b) ^ (a & c) ^ (b & c);
+}
+
+P1_HD uint32_t bsig0(uint32_t a) { return xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)); }
+P1_HD uint32_t bsig1(uint32_t e) { return xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)); }
+P1_HD uint32_t ssig0(uint32_t x) { return xor3(rotr(x, 7), rotr(x, 18), x >> 3); }
+P1_HD uint32_t ssig1(uint32_t x) { return xor3(rotr(x, 17), rotr(x, 19), x >> 10); }
+
+// Working variables a..h of one compression.
+struct State {
+  uint32_t v[8];
+};
+
+// One round with kw = K[t] + W[t] (either may be a compile-time constant).
+P1_HD void sha_round(State& s, uint32_t kw) {
+  const uint32_t a = s.v[0], b = s.v[1], c = s.v[2], d = s.v[3];
+  const uint32_t e = s.v[4], f = s.v[5], g = s.v[6], h = s.v[7];
+  const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kw;
+  const uint32_t t2 = bsig0(a) + maj(a, b, c);
+  s.v[7] = g; s.v[6] = f; s.v[5] = e; s.v[4] = d + t1;
+  s.v[3] = c; s.v[2] = b; s.v[1] = a; s.v[0] = t1 + t2;
+}
+
+// Message-schedule word t >= 16 of a 64-entry array (unrolled callers only).
+P1_HD uint32_t sched(const uint32_t* w, int t) {
+  return ssig1(w[t - 2]) + w[t - 7] + ssig0(w[t - 15]) + w[t - 16];
+}
+
+// Full compression of the block in w[0..15] chained into cv[8];
+// w[16..63] is scratch for the schedule.
+P1_HD void compress_full(uint32_t cv[8], uint32_t w[64]) {
+#pragma unroll
+  for (int t = 16; t < 64; ++t) w[t] = sched(w, t);
+  State s;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s.v[i] = cv[i];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) sha_round(s, k256(t) + w[t]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cv[i] += s.v[i];
+}
+
+}  // namespace p1

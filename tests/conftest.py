@@ -1,0 +1,38 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box)")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def oracle_mod():
+    import oracle
+
+    oracle.load()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """The HIP library, initialised on device 0.  Fails (not skips) when the
+    library or the device is missing: on the GPU box that is a real failure."""
+    import p1_amd
+
+    p1_amd.load()
+    p1_amd.init_devices([0])
+    return p1_amd

@@ -1,0 +1,108 @@
+"""Generate tests/golden/golden.json -- known-answer vectors for the scan.
+
+Run (container only, ~1 minute):  python tests/golden/make_golden.py
+Nothing here imports or runs the reference.  Sources of truth:
+  * p1.pdf section 4.1 (handout) known answers for bitcoin.Hash("msg", 0/1/2);
+  * expected results printed by the compiled staff tester
+    bin/linux_amd64/mtest ("Expecting result" lines), as recorded in
+    SURVEY.md section 8(c) -- data only, copied from the survey;
+  * everything else is computed here with Python's hashlib (an independent
+    SHA-256), restating hash.go:13-17 and miner.go:56-63:
+      Hash(m, n) = int.from_bytes(sha256(m + b" " + str(n)).digest()[:8], "big")
+      scan(m, lo, hi) = first strict minimum over lo..hi, identity (2^64-1, 0).
+"""
+import hashlib
+import json
+import os
+import random
+
+U64_MAX = (1 << 64) - 1
+
+
+def go_hash(m: bytes, n: int) -> int:
+    return int.from_bytes(hashlib.sha256(m + b" " + str(n).encode()).digest()[:8], "big")
+
+
+def go_scan(m: bytes, lo: int, hi: int):
+    best, bi = U64_MAX, 0
+    i = lo
+    while i <= hi:
+        h = go_hash(m, i)
+        if h < best:
+            best, bi = h, i
+        i += 1
+    return best, bi
+
+
+def main():
+    rnd = random.Random(440)
+    out = {"hash": [], "scan": []}
+
+    # handout KATs (p1.pdf 4.1, printed pp.13-14)
+    for n, want in [(0, 13781283048668101583), (1, 4754799531757243342), (2, 5611725180048225792)]:
+        assert go_hash(b"msg", n) == want
+        out["hash"].append({"msg_hex": b"msg".hex(), "nonce": n, "hash": want, "source": "p1.pdf 4.1"})
+    # handout scan example: Request("msg", 0, 2) -> Result(4754799531757243342, 1)
+    out["scan"].append({"msg_hex": b"msg".hex(), "lower": 0, "upper": 2, "hash": 4754799531757243342,
+                        "nonce": 1, "source": "p1.pdf 4.1"})
+
+    # compiled-reference vectors (mtest "Expecting result")
+    mtest = [("906262793464697609", 9999, 1455968979024161, 8439),
+             ("445404373034287280", 99999, 140966722763514, 54040),
+             ("365713827503619877", 999999, 22258228961853, 237918),
+             ("8212846827503921862", 9999999, 2878530887537, 5981267)]
+    for msg, mx, h, n in mtest:
+        if mx <= 99999:
+            assert go_scan(msg.encode(), 0, mx) == (h, n)
+        out["scan"].append({"msg_hex": msg.encode().hex(), "lower": 0, "upper": mx, "hash": h, "nonce": n,
+                            "source": "mtest (compiled reference) via SURVEY.md 8(c)"})
+
+    # survey hashlib result for configs[1] (full [0, 2^32-1], 8-process run)
+    out["scan"].append({"msg_hex": b"bradfitz".hex(), "lower": 0, "upper": (1 << 32) - 1,
+                        "hash": 5256245051, "nonce": 1626825724, "source": "SURVEY.md 8(c) hashlib",
+                        "large": True})
+
+    m120 = b"cmu440-p1-" * 12
+    named = [(b"bradfitz", 0, 9999), (b"", 0, 9999), (m120, 0, 9999),
+             (b"bradfitz", 10**9 - 5000, 10**9 + 5000), (b"bradfitz", 0, 0), (b"bradfitz", 7, 7),
+             (b"thom yorke", 19970521 - 1000, 19970521 + 1000), ("héllo".encode(), 0, 2000),
+             (b"msg", U64_MAX - 3000, U64_MAX), (b"bradfitz", 10**19 - 2000, 10**19 + 2000),
+             (b"bradfitz", 5, 3)]
+    for m, lo, hi in named:
+        h, n = go_scan(m, lo, hi)
+        out["scan"].append({"msg_hex": m.hex(), "lower": lo, "upper": hi, "hash": h, "nonce": n,
+                            "source": "hashlib"})
+
+    # Hash KATs over the tail-layout edge lengths x every digit count
+    lengths = [0, 1, 45, 46, 54, 55, 56, 57, 62, 63, 64, 119, 120, 1000, 1380]
+    for L in lengths:
+        m = bytes(rnd.randrange(32, 127) for _ in range(L))
+        for d in range(1, 21):
+            lo = 0 if d == 1 else 10 ** (d - 1)
+            hi = min(10 ** d - 1, U64_MAX)
+            n = rnd.randrange(lo, hi + 1)
+            out["hash"].append({"msg_hex": m.hex(), "nonce": n, "hash": go_hash(m, n), "source": "hashlib"})
+    for m, n in [(b"thom yorke", 19970521), (b"", 0), (b"msg", U64_MAX - 1), (b"msg", U64_MAX),
+                 (b"bradfitz", (1 << 32) - 1), ("héllo".encode(), 42), (m120, 0), (m120, (1 << 34) - 1)]:
+        out["hash"].append({"msg_hex": m.hex(), "nonce": n, "hash": go_hash(m, n), "source": "hashlib"})
+
+    # scan sweeps: every message length 0..130 and a few long ones, ranges
+    # that straddle a decade boundary (changes the tail layout mid-range)
+    for L in list(range(0, 131)) + [200, 255, 256, 1000, 1380]:
+        m = bytes(rnd.randrange(32, 127) for _ in range(L))
+        d = rnd.choice([4, 5, 6, 7, 8, 9, 10, 11, 12, 14, 16, 18, 19, 20])
+        b = 10 ** (d - 1)
+        lo = max(0, b - rnd.randrange(100, 2500))
+        hi = b + rnd.randrange(100, 2500)
+        h, n = go_scan(m, lo, hi)
+        out["scan"].append({"msg_hex": m.hex(), "lower": lo, "upper": hi, "hash": h, "nonce": n,
+                            "source": "hashlib"})
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=0)
+    print(f"wrote {path}: {len(out['hash'])} hash vectors, {len(out['scan'])} scan vectors")
+
+
+if __name__ == "__main__":
+    main()

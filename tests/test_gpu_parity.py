@@ -1,0 +1,136 @@
+"""GPU parity: libp1hip.so (through its C ABI) against the oracle and the
+golden fixtures.  Integer work -> bit-exact equality everywhere.
+
+Reference: miner.go:56-63 (scan), hash.go:13-17 (Hash)."""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+U64_MAX = (1 << 64) - 1
+M120 = b"cmu440-p1-" * 12
+
+
+def test_handout_kats(gpu):
+    assert gpu.hash("msg", 0) == 13781283048668101583
+    assert gpu.hash("msg", 1) == 4754799531757243342
+    assert gpu.hash("msg", 2) == 5611725180048225792
+    assert gpu.scan("msg", 0, 2) == (4754799531757243342, 1)
+
+
+def test_config1_client_answer(gpu):
+    # configs[0]: client 'bradfitz' maxNonce 9999 prints "Result 1419516646206828 9898"
+    assert gpu.scan("bradfitz", 0, 9999) == (1419516646206828, 9898)
+
+
+def test_golden_hashes(gpu, golden):
+    for v in golden["hash"]:
+        assert gpu.hash(bytes.fromhex(v["msg_hex"]), v["nonce"]) == v["hash"], v
+
+
+def test_golden_scans(gpu, golden):
+    for v in golden["scan"]:
+        got = gpu.scan(bytes.fromhex(v["msg_hex"]), v["lower"], v["upper"])
+        assert got == (v["hash"], v["nonce"]), v
+
+
+def test_config2_full_range(gpu):
+    # configs[1]: 'bradfitz', [0, 2^32) -- answer from SURVEY.md 8(c) (hashlib, 8 processes)
+    assert gpu.scan("bradfitz", 0, (1 << 32) - 1) == (5256245051, 1626825724)
+
+
+def test_every_layout_vs_oracle(gpu, oracle_mod):
+    rnd = random.Random(11)
+    for L in range(0, 130):
+        m = bytes(rnd.randrange(32, 127) for _ in range(L))
+        for d in (4, 7, 10, 11, 15, 20):
+            b = 10 ** (d - 1)
+            lo = b + rnd.randrange(0, 10**4) if d < 20 else b
+            hi = min(lo + rnd.randrange(1500, 4000), U64_MAX)
+            assert gpu.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
+
+
+def test_decade_straddles_vs_oracle(gpu, oracle_mod):
+    rnd = random.Random(12)
+    for L in (0, 8, 45, 54, 55, 62, 63, 64, 119, 120, 1000):
+        m = bytes(rnd.randrange(32, 127) for _ in range(L))
+        for d in range(2, 20):
+            b = 10 ** (d - 1)
+            lo, hi = max(0, b - 1234), b + 2345
+            assert gpu.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (L, d)
+
+
+def test_larger_ranges_vs_oracle(gpu, oracle_mod):
+    for m, lo, hi in [(b"bradfitz", 0, 999_999), (M120, 10**9 - 500_000, 10**9 + 500_000),
+                      (b"x" * 55, 12_345_678, 13_045_678), (b"", 0, 1_000_000)]:
+        assert gpu.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (m[:8], lo, hi)
+
+
+def test_edges(gpu, oracle_mod):
+    assert gpu.scan("bradfitz", 5, 3) == (U64_MAX, 0)            # Lower > Upper
+    assert gpu.scan("bradfitz", 0, 0) == (oracle_mod.hash("bradfitz", 0), 0)
+    assert gpu.scan(b"", 7, 7) == (oracle_mod.hash(b"", 7), 7)
+    for lo in (U64_MAX - 3000, U64_MAX):                           # no wrap at 2^64-1
+        assert gpu.scan("msg", lo, U64_MAX) == oracle_mod.scan("msg", lo, U64_MAX, threads=8)
+    big = bytes(range(256)) * 6                                     # 1536 B, > LSP frame
+    assert gpu.scan(big, 10**12, 10**12 + 3000) == oracle_mod.scan(big, 10**12, 10**12 + 3000, threads=8)
+    utf8 = "héllo wörld ✓".encode()
+    assert gpu.scan(utf8, 0, 5000) == oracle_mod.scan(utf8, 0, 5000, threads=8)
+
+
+def test_tie_breaking_reduction(gpu):
+    rnd = random.Random(5)
+    # equal minimum hashes: lowest nonce wins (strict '<' at miner.go:59)
+    n = 100_000
+    hs = [rnd.randrange(1 << 40, U64_MAX) for _ in range(n)]
+    ns = list(range(10**6, 10**6 + n))
+    rnd.shuffle(ns)
+    pos = rnd.sample(range(n), 7)
+    for p in pos:
+        hs[p] = 12345
+    want = (12345, min(ns[p] for p in pos))
+    assert gpu.reduce_pairs(hs, ns) == want
+    # ties inside one wave and across waves / workgroups
+    for size in (1, 2, 63, 64, 65, 255, 256, 257, 4097):
+        hs = [7] * size
+        ns = list(range(size, 0, -1))
+        assert gpu.reduce_pairs(hs, ns) == (7, 1)
+    # identity rules
+    assert gpu.reduce_pairs([], []) == (U64_MAX, 0)
+    assert gpu.reduce_pairs([U64_MAX] * 300, list(range(5, 305))) == (U64_MAX, 0)
+    assert gpu.reduce_pairs([U64_MAX, U64_MAX - 1], [1, 99]) == (U64_MAX - 1, 99)
+
+
+def test_full_size_properties_config3(gpu, oracle_mod):
+    """configs[2] (120-byte msg, [0, 2^34)) is too big for the CPU oracle, so
+    check size-independent properties: the reported nonce re-hashes to the
+    reported hash, and the scan is the min of its two halves (split at an
+    arbitrary point), each of which also re-hashes."""
+    hi = (1 << 34) - 1
+    h, n = gpu.scan(M120, 0, hi)
+    assert 0 <= n <= hi and oracle_mod.hash(M120, n) == h
+    cut = 9_876_543_210
+    a = gpu.scan(M120, 0, cut)
+    b = gpu.scan(M120, cut + 1, hi)
+    assert min(a, b) == (h, n)
+    for hh, nn in (a, b):
+        assert oracle_mod.hash(M120, nn) == hh
+
+
+def test_stats_and_profiling(gpu):
+    gpu.reset_stats()
+    gpu.set_profiling(True)
+    gpu.scan("bradfitz", 0, 10**8)
+    s = gpu.get_stats()
+    gpu.set_profiling(False)
+    assert s["scans"] == 1 and s["fast_launches"] >= 1
+    assert s["fast_nonces"] + s["generic_nonces"] == 10**8 + 1
+    assert s["fast_kernel_ms"] > 0
+    assert s["fast_alg_ops"] == 1384 * s["fast_nonces"]  # 'bradfitz' is 1 block per nonce
+
+
+def test_init_variants(gpu):
+    got = gpu.init(1)
+    assert got == 1 and gpu.device_count() == 1
+    gpu.init_devices([0])
+    assert gpu.scan("msg", 0, 2) == (4754799531757243342, 1)

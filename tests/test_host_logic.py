@@ -1,0 +1,162 @@
+"""CPU tests of the host logic: the planner + the kernels' per-thread code
+replayed on the host by tools/p1emu (layout coverage without a GPU), the
+C-ABI library's exports, and the sharding/combine rules of the multi-GPU
+path."""
+import os
+import random
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+U64_MAX = (1 << 64) - 1
+EMU = os.path.join(ROOT, "tools", "p1emu")
+
+
+def emu(msg, lo, hi, generic=False):
+    args = [EMU, msg.hex() if msg else "-", str(lo), str(hi)] + (["generic"] if generic else [])
+    out = subprocess.run(args, capture_output=True, text=True, check=True).stdout.split()
+    return (int(out[0]), int(out[1])), int(out[2]), int(out[3])
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    if not os.path.exists(EMU):
+        subprocess.run(["make", "-s", "-C", ROOT, "tools/p1emu"], check=True)
+
+
+def test_emu_golden_scans(golden):
+    n_fast = 0
+    for v in golden["scan"]:
+        if v.get("large") or v["upper"] - v["lower"] > 200000:
+            continue
+        got, nf, _ = emu(bytes.fromhex(v["msg_hex"]), v["lower"], v["upper"])
+        n_fast += nf
+        assert got == (v["hash"], v["nonce"]), v
+    assert n_fast > 50  # the fast (per-thread 10^k loop) path was exercised
+
+
+def test_emu_generic_only_matches(golden):
+    for v in golden["scan"][:40]:
+        if v.get("large") or v["upper"] - v["lower"] > 20000:
+            continue
+        got, nf, ng = emu(bytes.fromhex(v["msg_hex"]), v["lower"], v["upper"], generic=True)
+        assert nf == 0
+        assert got == (v["hash"], v["nonce"]), v
+
+
+def test_emu_every_layout(oracle_mod):
+    """Every prefix length mod 64 x several digit counts: hits every
+    (FV, NV, TRAIL) variant, PRE blocks and the k=1/2 straddle case."""
+    rnd = random.Random(7)
+    for L in range(0, 128):
+        m = bytes(rnd.randrange(32, 127) for _ in range(L))
+        for d in (5, 9, 10, 11, 20):
+            b = 10 ** (d - 1)
+            lo = b + rnd.randrange(0, 10**4)
+            hi = min(lo + 1999, U64_MAX)
+            got, nf, _ = emu(m, lo, hi)
+            assert nf >= 1
+            assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
+
+
+def test_emu_range_top(oracle_mod):
+    for m in (b"msg", b"x" * 60):
+        got, _, _ = emu(m, U64_MAX - 2500, U64_MAX)
+        assert got == oracle_mod.scan(m, U64_MAX - 2500, U64_MAX, threads=8)
+
+
+def test_emu_empty_range():
+    got, nf, ng = emu(b"bradfitz", 10, 9)
+    assert got == (U64_MAX, 0) and nf == 0 and ng == 0
+
+
+def _header_symbols():
+    with open(os.path.join(ROOT, "include", "p1hip.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(p1hip_[a-z_]+)\s*\(", text)))
+
+
+def test_capi_exports_every_header_symbol():
+    """libp1hip.so loads on a CPU-only host and exports every declared entry
+    point (no compute call is made here)."""
+    import ctypes
+
+    import p1_amd
+    from p1_amd import _lib
+
+    lib = ctypes.CDLL(p1_amd.lib_path())
+    syms = _header_symbols()
+    assert len(syms) >= 12
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(n for n, _, _ in _lib.SIGNATURES) == syms
+    assert p1_amd.version().startswith("p1hip")
+
+
+def test_capi_no_device_fails_loudly():
+    """Without a GPU the product path raises; it never falls back to a CPU hash."""
+    import p1_amd
+
+    try:
+        import torch
+
+        if torch.cuda.device_count() > 0:
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    with pytest.raises(p1_amd.P1HipError) as ei:
+        p1_amd.scan("bradfitz", 0, 10)
+    assert ei.value.rc == -1
+
+
+def test_capi_bad_args():
+    import ctypes
+
+    import p1_amd
+
+    lib = p1_amd.load()
+    h, n = ctypes.c_uint64(), ctypes.c_uint64()
+    assert lib.p1hip_scan(None, 5, 0, 1, ctypes.byref(h), ctypes.byref(n)) == -4
+    assert lib.p1hip_scan(b"x", (1 << 28) + 1, 0, 1, ctypes.byref(h), ctypes.byref(n)) == -4
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_range_covers(world):
+    from p1_amd import shard_range
+
+    for lo, hi in [(0, 0), (0, 9), (5, 3), (0, (1 << 32) - 1), (U64_MAX - 5, U64_MAX), (0, U64_MAX)]:
+        shards = [shard_range(lo, hi, r, world) for r in range(world)]
+        got = [s for s in shards if s is not None]
+        if lo > hi:
+            assert not got
+            continue
+        assert got[0][0] == lo and got[-1][1] == hi
+        for a, b in zip(got, got[1:]):
+            assert b[0] == a[1] + 1
+        sizes = [b - a + 1 for a, b in got]
+        assert max(sizes) - min(sizes) <= 1
+
+
+def test_combine_keys_rules():
+    from p1_amd import combine_keys
+
+    assert combine_keys([]) == (U64_MAX, 0)
+    assert combine_keys([(U64_MAX, 0), (U64_MAX, 0)]) == (U64_MAX, 0)
+    assert combine_keys([(5, 9), (5, 3), (7, 1)]) == (5, 3)
+    assert combine_keys([(U64_MAX, 0), (U64_MAX - 1, 12)]) == (U64_MAX - 1, 12)
+
+
+def test_sharded_oracle_equals_serial(oracle_mod):
+    from p1_amd import combine_keys, shard_range
+
+    for world in (2, 4, 8):
+        for lo, hi in [(0, 9999), (10**9 - 3000, 10**9 + 3000)]:
+            keys = []
+            for r in range(world):
+                s = shard_range(lo, hi, r, world)
+                if s:
+                    keys.append(oracle_mod.scan("bradfitz", s[0], s[1]))
+            assert combine_keys(keys) == oracle_mod.scan("bradfitz", lo, hi)
