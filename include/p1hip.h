@@ -86,10 +86,16 @@ typedef struct {
   uint64_t fast_nonces;     /* nonces hashed by those launches                    */
   uint64_t fast_alg_ops;    /* algorithmic int32 ops: 1384 * B_tail per nonce     */
   double fast_kernel_ms;    /* sum of HIP-event durations of those launches
-                               (only while profiling is on, else 0)               */
+                               (only while profiling is on, else 0); launches
+                               of one scan may overlap on the device's streams  */
   uint64_t generic_launches;/* launches of the generic (edge) kernel              */
   uint64_t generic_nonces;  /* nonces hashed by the generic kernel                */
   double scan_wall_ms;      /* host wall time inside p1hip_scan                   */
+  /* the largest fast launch of each scan ("dominant kernel" for the roofline) */
+  uint64_t dom_launches;
+  uint64_t dom_nonces;
+  uint64_t dom_alg_ops;
+  double dom_kernel_ms;     /* HIP-event durations (profiling on)                 */
 } p1hip_stats_t;
 
 /* Record HIP events (on the library's own stream) around every fast-kernel

@@ -28,6 +28,10 @@ class Stats(ctypes.Structure):
         ("generic_launches", U64),
         ("generic_nonces", U64),
         ("scan_wall_ms", ctypes.c_double),
+        ("dom_launches", U64),
+        ("dom_nonces", U64),
+        ("dom_alg_ops", U64),
+        ("dom_kernel_ms", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -35,7 +39,9 @@ class Stats(ctypes.Structure):
 
 
 def lib_path():
-    return os.path.join(_HERE, "libp1hip.so")
+    # P1HIP_LIB selects an alternative build of the same library (A/B tuning
+    # builds under p1_amd/variants/); default is the in-tree libp1hip.so.
+    return os.environ.get("P1HIP_LIB") or os.path.join(_HERE, "libp1hip.so")
 
 
 # (name, restype, argtypes) for every entry point of include/p1hip.h

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <mutex>
 #include <string>
@@ -91,8 +92,14 @@ __device__ __forceinline__ void block_min_store(Key k, Key* out) {
 // ----------------------------------------------------------------------------
 // Kernels
 // ----------------------------------------------------------------------------
+// Minimum waves per SIMD the register allocator must leave room for
+// (tuned on MI355X); override with -DP1_FAST_WAVES=n.
+#ifndef P1_FAST_WAVES
+#define P1_FAST_WAVES 5
+#endif
+
 template <int FV, int NV, bool TRAIL>
-__global__ __launch_bounds__(kBlock) void k_scan_fast(const FastArgs A, Key* __restrict__ part) {
+__global__ __launch_bounds__(kBlock, P1_FAST_WAVES) void k_scan_fast(const FastArgs A, Key* __restrict__ part) {
   const Key k = fast_thread<FV, NV, TRAIL>(A, blockIdx.x * kBlock + threadIdx.x);
   block_min_store<kBlock>(k, part + A.part_off + blockIdx.x);
 }
@@ -156,9 +163,16 @@ int fail(int rc, const std::string& what) {
       return fail(P1HIP_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_));      \
   } while (0)
 
+// Launches of one scan are spread over kStreams streams (largest first) so
+// that the drain of one decade's grid overlaps the next one's work; the
+// reduction waits for all of them on the main stream.
+constexpr int kStreams = 4;
+
 struct Dev {
   int ordinal = -1;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;            // main stream (= streams[0])
+  hipStream_t aux[kStreams - 1] = {};      // streams[1..]
+  hipEvent_t join[kStreams - 1] = {};      // aux -> main dependencies
   Key* d_part = nullptr;
   size_t part_cap = 0;
   Key* d_res = nullptr;     // 1 Key
@@ -169,6 +183,9 @@ struct Dev {
   // per-scan accounting filled by run_plan
   uint64_t fast_launches = 0, fast_nonces = 0, fast_ops = 0, gen_launches = 0, gen_nonces = 0;
   double fast_ms = 0.0;
+  uint64_t dom_nonces = 0, dom_ops = 0;  // largest fast launch of the scan
+  double dom_ms = 0.0;
+  hipStream_t pick(int i) const { return i == 0 ? stream : aux[i - 1]; }
 };
 
 struct Runtime {
@@ -189,6 +206,10 @@ int dev_release(Dev& d) {
   if (d.stream) (void)hipStreamSynchronize(d.stream);
   for (hipEvent_t e : d.evs) (void)hipEventDestroy(e);
   d.evs.clear();
+  for (int i = 0; i < kStreams - 1; ++i) {
+    if (d.join[i]) (void)hipEventDestroy(d.join[i]);
+    if (d.aux[i]) (void)hipStreamDestroy(d.aux[i]);
+  }
   if (d.comm) ncclCommDestroy(d.comm);
   if (d.d_part) (void)hipFree(d.d_part);
   if (d.d_res) (void)hipFree(d.d_res);
@@ -228,6 +249,10 @@ int init_locked(Runtime& R, const std::vector<int>& ords) {
     d.ordinal = ords[i];
     HIPCHK(hipSetDevice(d.ordinal));
     HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    for (int j = 0; j < kStreams - 1; ++j) {
+      HIPCHK(hipStreamCreateWithFlags(&d.aux[j], hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&d.join[j], hipEventDisableTiming));
+    }
     HIPCHK(hipMalloc(&d.d_res, sizeof(Key)));
     HIPCHK(hipMalloc(&d.d_gather, sizeof(Key) * nd));
     HIPCHK(hipHostMalloc(&d.h_res, sizeof(Key) * nd, hipHostMallocDefault));
@@ -254,7 +279,8 @@ int ensure_init(Runtime& R) {
 int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, bool profiling) {
   HIPCHK(hipSetDevice(d.ordinal));
   d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
-  d.fast_ms = 0.0;
+  d.dom_nonces = d.dom_ops = 0;
+  d.fast_ms = d.dom_ms = 0.0;
   Plan plan;
   std::string err = make_plan(msg, len, lo, hi, plan);
   if (!err.empty()) return fail(P1HIP_ERR_ARGS, "planner: " + err);
@@ -266,8 +292,21 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
     HIPCHK(hipMalloc(&d.d_part, cap * sizeof(Key)));
     d.part_cap = cap;
   }
+  // largest launches first, dealt round-robin over the streams
+  std::vector<size_t> order(plan.launches.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+    return plan.launches[a].nonces * plan.launches[a].btail > plan.launches[b].nonces * plan.launches[b].btail;
+  });
+  const size_t dom = order.empty() ? 0 : order[0];
+  std::vector<size_t> ev_launch;  // launch index of each timed event pair
   size_t nev = 0;
-  for (const Launch& L : plan.launches) {
+  int used = 1;
+  for (size_t r = 0; r < order.size(); ++r) {
+    const Launch& L = plan.launches[order[r]];
+    const int si = (int)(r % kStreams);
+    hipStream_t st = d.pick(si);
+    if (si + 1 > used) used = si + 1;
     if (L.fast) {
       FastKernel fn = fast_kernel(L.fv, L.nv, L.trail);
       if (!fn) return fail(P1HIP_ERR_ARGS, "no fast kernel variant");
@@ -277,33 +316,43 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
           HIPCHK(hipEventCreate(&e));
           d.evs.push_back(e);
         }
-        HIPCHK(hipEventRecord(d.evs[nev], d.stream));
+        HIPCHK(hipEventRecord(d.evs[nev], st));
       }
-      hipLaunchKernelGGL(fn, dim3(L.blocks), dim3(kBlock), 0, d.stream, L.fa, d.d_part);
+      hipLaunchKernelGGL(fn, dim3(L.blocks), dim3(kBlock), 0, st, L.fa, d.d_part);
       HIPCHK(hipGetLastError());
       if (profiling) {
-        HIPCHK(hipEventRecord(d.evs[nev + 1], d.stream));
+        HIPCHK(hipEventRecord(d.evs[nev + 1], st));
+        ev_launch.push_back(order[r]);
         nev += 2;
       }
       d.fast_launches++;
       d.fast_nonces += L.nonces;
       d.fast_ops += L.nonces * kAlgOpsPerCompression * (uint64_t)L.btail;
+      if (order[r] == dom) {
+        d.dom_nonces += L.nonces;
+        d.dom_ops += L.nonces * kAlgOpsPerCompression * (uint64_t)L.btail;
+      }
     } else {
-      hipLaunchKernelGGL(k_scan_generic, dim3(L.blocks), dim3(kBlock), 0, d.stream, L.ga, d.d_part);
+      hipLaunchKernelGGL(k_scan_generic, dim3(L.blocks), dim3(kBlock), 0, st, L.ga, d.d_part);
       HIPCHK(hipGetLastError());
       d.gen_launches++;
       d.gen_nonces += L.nonces;
     }
   }
+  for (int j = 1; j < used; ++j) {
+    HIPCHK(hipEventRecord(d.join[j - 1], d.aux[j - 1]));
+    HIPCHK(hipStreamWaitEvent(d.stream, d.join[j - 1], 0));
+  }
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, d.stream, d.d_part, plan.total_blocks,
                      d.d_res);
   HIPCHK(hipGetLastError());
   if (profiling && nev) {
-    HIPCHK(hipEventSynchronize(d.evs[nev - 1]));
     for (size_t i = 0; i < nev; i += 2) {
+      HIPCHK(hipEventSynchronize(d.evs[i + 1]));
       float ms = 0.f;
       HIPCHK(hipEventElapsedTime(&ms, d.evs[i], d.evs[i + 1]));
       d.fast_ms += ms;
+      if (ev_launch[i / 2] == dom) d.dom_ms += ms;
     }
   }
   return P1HIP_OK;
@@ -424,6 +473,10 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
       R.stats.fast_kernel_ms += d.fast_ms;
       R.stats.generic_launches += d.gen_launches;
       R.stats.generic_nonces += d.gen_nonces;
+      if (d.dom_nonces) R.stats.dom_launches++;
+      R.stats.dom_nonces += d.dom_nonces;
+      R.stats.dom_alg_ops += d.dom_ops;
+      R.stats.dom_kernel_ms += d.dom_ms;
     }
   }
   R.stats.scans++;

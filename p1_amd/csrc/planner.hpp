@@ -29,6 +29,10 @@ namespace p1 {
 constexpr uint64_t kMaxFastThreads = 1ull << 24;   // hi values per fast launch
 constexpr uint64_t kMaxGenericThreads = 1ull << 24; // nonces per generic launch
 constexpr uint64_t kAlgOpsPerCompression = 1384;
+// A fast launch wants >= 4 waves on each of the 1024 SIMDs; decades too small
+// for that at k = 3 drop to k = 2 or 1 (shorter per-thread loops, more threads)
+// instead of running a few long waves on a mostly idle chip.
+constexpr uint64_t kMinFastThreads = 1ull << 18;
 
 inline uint64_t pow10u(int e) {
   uint64_t v = 1;
@@ -157,7 +161,7 @@ inline void add_generic(const Prefix& P, const Layout& Y, uint64_t s, uint64_t e
 
 // Returns an empty string on success, else a description of the problem.
 inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint64_t he, Plan& plan) {
-  const int k = Y.k;
+  const int k = Y.k;  // may be below make_layout's choice (see make_plan)
   const int qv = Y.q - 64 * Y.vb;          // last digit inside the variable block
   const int fv = (qv - k + 1) >> 2;
   const int jl = qv >> 2;
@@ -239,7 +243,10 @@ inline std::string make_plan(const uint8_t* msg, size_t L, uint64_t lower, uint6
     const uint64_t s = lower > dlo ? lower : dlo;
     const uint64_t e = upper < dhi ? upper : dhi;
     if (s > e) continue;
-    const Layout Y = make_layout(P.r, d);
+    Layout Y = make_layout(P.r, d);
+    // smaller k keeps the lo digits inside the same block (they are a suffix
+    // of make_layout's k digits), so any k <= Y.k is a valid layout
+    while (Y.k > 1 && (e - s) / pow10u(Y.k) + 1 < kMinFastThreads) --Y.k;
     if (!fast_ok || d <= Y.k) {
       add_generic(P, Y, s, e, plan);
       continue;

@@ -116,32 +116,64 @@ P1_HD void place_digits(const uint32_t* tmpl, uint64_t x, uint32_t ndig, uint32_
 //                               FV+NV         uniform (pad byte or 0)
 //                               > FV+NV       0, except W15 = bit length
 //                                             when !TRAIL (host-checked)
+// Everything that does not depend on the per-nonce words is computed once
+// per thread before the loop (explicitly: the bitop3 asm is convergent, so
+// the compiler would not hoist it): rounds 0..FV-1, the invariant half of
+// round FV, every invariant schedule word (as K[t]+W[t]) and the invariant
+// part of every variant schedule word.
 // ---------------------------------------------------------------------------
+
+// Bit t set <=> schedule word t depends on the per-nonce words.
+P1_HD constexpr uint64_t var_mask(int fv, int nv) {
+  uint64_t m = 0;
+  for (int t = 0; t < 64; ++t) {
+    bool v;
+    if (t < 16) v = (t >= fv && t < fv + nv);
+    else v = ((m >> (t - 2)) & 1) || ((m >> (t - 7)) & 1) || ((m >> (t - 15)) & 1) || ((m >> (t - 16)) & 1);
+    if (v) m |= 1ull << t;
+  }
+  return m;
+}
+
 template <int FV, int NV, bool TRAIL>
-P1_HD uint64_t fast_tail_hash(const State& s_fv, const uint32_t cv[8], const uint32_t Wt[16],
-                              uint32_t wv0, uint32_t wv1, uint32_t wu, uint32_t wlen,
-                              const uint32_t* kw2) {
+struct FastPre {
+  static constexpr uint64_t kVar = var_mask(FV, NV);
+  P1_HD static constexpr bool var(int t) { return (kVar >> t) & 1; }
+  uint32_t cv[8];   // chaining value entering the variable block
+  uint32_t kw[64];  // !var(t): K[t] + W[t];   var(t), t >= 16: invariant partial sum of W[t]
+  uint32_t wI[16];  // invariant message words (valid where !var)
+  State s1;         // state after round FV, minus the per-nonce word:
+                    //   a = s1.v[0] + W[FV], e = s1.v[4] + W[FV], rest as is
+};
+
+template <int FV, int NV, bool TRAIL>
+P1_HD uint64_t fast_hash(const FastPre<FV, NV, TRAIL>& P, uint32_t wv0, uint32_t wv1, const uint32_t* kw2) {
+  using FP = FastPre<FV, NV, TRAIL>;
   uint32_t w[64];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    if (i < FV) w[i] = Wt[i];
-    else if (i == FV) w[i] = wv0;
-    else if (NV == 2 && i == FV + 1) w[i] = wv1;
-    else if (i == FV + NV) w[i] = wu;
-    else if (!TRAIL && i == 15) w[i] = wlen;
-    else w[i] = 0u;
+  for (int i = 0; i < 16; ++i) w[i] = (i == FV) ? wv0 : (NV == 2 && i == FV + 1) ? wv1 : P.wI[i];
+#pragma unroll
+  for (int t = 16; t < 64; ++t) {
+    if (FP::var(t)) {
+      uint32_t v = P.kw[t];
+      if (FP::var(t - 2)) v += ssig1(w[t - 2]);
+      if (FP::var(t - 7)) v += w[t - 7];
+      if (FP::var(t - 15)) v += ssig0(w[t - 15]);
+      if (FP::var(t - 16)) v += w[t - 16];
+      w[t] = v;
+    }
   }
+  State s = P.s1;
+  s.v[0] += wv0;  // round FV, per-nonce half
+  s.v[4] += wv0;
 #pragma unroll
-  for (int t = 16; t < 64; ++t) w[t] = sched(w, t);
-  State s = s_fv;
-#pragma unroll
-  for (int t = FV; t < 64; ++t) sha_round(s, k256(t) + w[t]);
+  for (int t = FV + 1; t < 64; ++t) sha_round(s, FP::var(t) ? k256(t) + w[t] : P.kw[t]);
   if constexpr (!TRAIL) {
-    return ((uint64_t)(cv[0] + s.v[0]) << 32) | (uint64_t)(cv[1] + s.v[1]);
+    return ((uint64_t)(P.cv[0] + s.v[0]) << 32) | (uint64_t)(P.cv[1] + s.v[1]);
   } else {
     uint32_t cv2[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) cv2[i] = cv[i] + s.v[i];
+    for (int i = 0; i < 8; ++i) cv2[i] = P.cv[i] + s.v[i];
     State s2;
 #pragma unroll
     for (int i = 0; i < 8; ++i) s2.v[i] = cv2[i];
@@ -153,21 +185,22 @@ P1_HD uint64_t fast_tail_hash(const State& s_fv, const uint32_t cv[8], const uin
 
 template <int FV, int NV, bool TRAIL>
 P1_HD Key fast_thread(const FastArgs& A, uint32_t tid) {
+  using FP = FastPre<FV, NV, TRAIL>;
   const bool valid = tid < A.nthreads;
   const uint64_t hi = A.hi_first + (valid ? tid : 0u);
 
   uint32_t T[32];
   place_digits(A.tmpl, hi, A.dh, A.p_last, T);
 
-  uint32_t cv[8];
+  FP P;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) cv[i] = A.mid[i];
+  for (int i = 0; i < 8; ++i) P.cv[i] = A.mid[i];
   const bool pre = A.pre != 0;
   if (pre) {  // tail block 0 holds only prefix bytes and hi digits
     uint32_t w[64];
 #pragma unroll
     for (int i = 0; i < 16; ++i) w[i] = T[i];
-    compress_full(cv, w);
+    compress_full(P.cv, w);
   }
   // variable block = tail block `pre`; a mask blend (not a select) keeps the
   // compiler from lowering this to a runtime-indexed scratch array
@@ -177,13 +210,51 @@ P1_HD Key fast_thread(const FastArgs& A, uint32_t tid) {
   for (int i = 0; i < 16; ++i) Wt[i] = (T[i] & ~pm) | (T[16 + i] & pm);
   const uint32_t wu = (FV + NV < 16) ? (pre ? A.tmpl[16 + FV + NV] : A.tmpl[FV + NV]) : 0u;
   const uint32_t wlen = pre ? A.tmpl[31] : A.tmpl[15];
-
-  // rounds 0..FV-1 see only thread-constant words
-  State s_fv;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s_fv.v[i] = cv[i];
+  for (int i = 0; i < 16; ++i) {
+    if (i < FV) P.wI[i] = Wt[i];
+    else if (i < FV + NV) P.wI[i] = 0u;  // per-nonce word (never read as invariant)
+    else if (i == FV + NV) P.wI[i] = wu;
+    else if (!TRAIL && i == 15) P.wI[i] = wlen;
+    else P.wI[i] = 0u;
+  }
+  // invariant schedule: full words where !var, partial sums where var
+  {
+    uint32_t wi[64];
 #pragma unroll
-  for (int t = 0; t < FV; ++t) sha_round(s_fv, k256(t) + Wt[t]);
+    for (int i = 0; i < 16; ++i) wi[i] = P.wI[i];
+#pragma unroll
+    for (int t = 16; t < 64; ++t) {
+      if (!FP::var(t)) {
+        wi[t] = sched(wi, t);
+      } else {
+        uint32_t v = 0;
+        if (!FP::var(t - 2)) v += ssig1(wi[t - 2]);
+        if (!FP::var(t - 7)) v += wi[t - 7];
+        if (!FP::var(t - 15)) v += ssig0(wi[t - 15]);
+        if (!FP::var(t - 16)) v += wi[t - 16];
+        wi[t] = 0u;
+        P.kw[t] = v;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 64; ++t)
+      if (!FP::var(t)) P.kw[t] = k256(t) + wi[t];
+  }
+  // rounds 0..FV-1 and the invariant half of round FV
+  State s;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s.v[i] = P.cv[i];
+#pragma unroll
+  for (int t = 0; t < FV; ++t) sha_round(s, P.kw[t]);
+  {
+    const uint32_t a = s.v[0], b = s.v[1], c = s.v[2], d = s.v[3];
+    const uint32_t e = s.v[4], f = s.v[5], g = s.v[6], h = s.v[7];
+    const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + k256(FV);  // + W[FV] per nonce
+    const uint32_t t2 = bsig0(a) + maj(a, b, c);
+    P.s1.v[0] = t1 + t2; P.s1.v[1] = a; P.s1.v[2] = b; P.s1.v[3] = c;
+    P.s1.v[4] = d + t1;  P.s1.v[5] = e; P.s1.v[6] = f; P.s1.v[7] = g;
+  }
 
   uint32_t wv0 = Wt[FV];
   uint32_t wv1 = (NV == 2) ? Wt[FV + 1] : 0u;
@@ -193,7 +264,7 @@ P1_HD Key fast_thread(const FastArgs& A, uint32_t tid) {
   for (uint32_t c2 = 0; c2 < A.n2; ++c2) {
     for (uint32_t c1 = 0; c1 < A.n1; ++c1) {
       for (uint32_t c0 = 0; c0 < 10u; ++c0) {
-        const uint64_t h = fast_tail_hash<FV, NV, TRAIL>(s_fv, cv, Wt, wv0, wv1, wu, wlen, A.kw2);
+        const uint64_t h = fast_hash<FV, NV, TRAIL>(P, wv0, wv1, A.kw2);
         const bool lt = h < best;  // strict '<': first minimum wins (miner.go:59)
         best = lt ? h : best;
         bestc = lt ? c : bestc;

@@ -1,0 +1,97 @@
+// p1miner -- the miner's Request -> Result loop (miner.go:49-67) over stdio,
+// GPU-backed through libp1hip.so.  The LSP transport (SRC/lsp) is out of
+// scope; requests/results are the same encoding/json bitcoin.Message bytes
+// the reference puts in LSP payloads (miner.go:55,66).
+//
+//   p1miner scan <msg> <lower> <upper>   prints "Result <hash> <nonce>"
+//                                        (the client's output, client.go:59-61)
+//   p1miner hash <msg> <nonce>           prints bitcoin.Hash(msg, nonce)
+//   p1miner serve [--device N] [--chunk C]
+//                                        one JSON Message per stdin line; every
+//                                        Request is answered with one JSON
+//                                        Result line (Join/Result lines ignored)
+//   p1miner json                         re-marshals stdin JSON lines (no GPU;
+//                                        wire-format tests)
+#include <errno.h>
+#include <inttypes.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <iostream>
+#include <string>
+
+#include "../../include/p1hip.h"
+#include "bitcoin.hpp"
+
+static int usage() {
+  fprintf(stderr,
+          "usage: p1miner scan <msg> <lower> <upper> | hash <msg> <nonce> | "
+          "serve [--device N] [--chunk C] | json\n");
+  return 2;
+}
+
+static bool parse_u64(const char* s, uint64_t* v) {
+  char* end = nullptr;
+  if (!s || !*s || *s == '-') return false;
+  errno = 0;
+  unsigned long long r = strtoull(s, &end, 10);
+  if (errno || *end) return false;
+  *v = r;
+  return true;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) return usage();
+  const std::string cmd = argv[1];
+  try {
+    if (cmd == "scan" && argc == 5) {
+      uint64_t lo, hi, h, n;
+      if (!parse_u64(argv[3], &lo) || !parse_u64(argv[4], &hi)) return usage();
+      miner::ScanChunked(argv[2], lo, hi, miner::kDefaultChunk, &h, &n);
+      printf("Result %" PRIu64 " %" PRIu64 "\n", h, n);
+      return 0;
+    }
+    if (cmd == "hash" && argc == 4) {
+      uint64_t n;
+      if (!parse_u64(argv[3], &n)) return usage();
+      printf("%" PRIu64 "\n", bitcoin::Hash(argv[2], n));
+      return 0;
+    }
+    if (cmd == "json") {
+      std::string line;
+      while (std::getline(std::cin, line)) {
+        bitcoin::Message m;
+        if (!bitcoin::Unmarshal(line, &m)) { printf("ERROR\n"); continue; }
+        printf("%s\t%s\n", bitcoin::Marshal(m).c_str(), m.String().c_str());
+      }
+      return 0;
+    }
+    if (cmd == "serve") {
+      int dev = -1;
+      uint64_t chunk = miner::kDefaultChunk;
+      for (int i = 2; i < argc; ++i) {
+        if (!strcmp(argv[i], "--device") && i + 1 < argc) dev = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--chunk") && i + 1 < argc) { if (!parse_u64(argv[++i], &chunk)) return usage(); }
+        else return usage();
+      }
+      int rc = dev >= 0 ? p1hip_init_devices(&dev, 1) : p1hip_init(0, nullptr);
+      if (rc != P1HIP_OK) { fprintf(stderr, "p1hip init: %s\n", p1hip_last_error()); return 1; }
+      std::string line;
+      while (std::getline(std::cin, line)) {
+        bitcoin::Message req;
+        if (!bitcoin::Unmarshal(line, &req)) continue;  // miner.go:55 ignores decode errors
+        if (req.Type != bitcoin::Request) continue;
+        bitcoin::Message res = miner::HandleRequest(req, chunk);
+        printf("%s\n", bitcoin::Marshal(res).c_str());
+        fflush(stdout);
+      }
+      p1hip_shutdown();
+      return 0;
+    }
+  } catch (const bitcoin::HipError& e) {
+    fprintf(stderr, "%s\n", e.what());
+    return 1;
+  }
+  return usage();
+}

@@ -1,0 +1,80 @@
+"""The C++ host mirror of the reference's bitcoin package / miner loop
+(p1_amd/host, binary p1_amd/p1miner)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+MINER = os.path.join(ROOT, "p1_amd", "p1miner")
+U64_MAX = (1 << 64) - 1
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    if not os.path.exists(MINER):
+        subprocess.run(["make", "-s", "-C", ROOT, "p1_amd/p1miner"], check=True)
+
+
+def run(args, stdin=None):
+    return subprocess.run([MINER] + args, input=stdin, capture_output=True, text=True, timeout=600)
+
+
+def test_json_wire_format_matches_go():
+    # Go encoding/json of bitcoin.Message (message.go:18-23): field order,
+    # HTML-safe escaping (< > &), uint64 as exact integers.
+    lines = [
+        '{"Type":1,"Data":"bradfitz","Lower":0,"Upper":9999,"Hash":0,"Nonce":0}',
+        '{"type":2,"hash":18446744073709551615,"nonce":5}',       # Go matches keys case-insensitively
+        '{"Type":1,"Data":"a<b>&\\"c\\\\ \\u00e9\\u0001\\n","Lower":1,"Upper":2}',
+        '{"Type":0,"Extra":[1,{"x":null}],"Data":null}',          # unknown keys / null ignored
+        '{"Type":1,"Lower":-1}',                                  # negative uint64 rejected
+        '{"Type":1,"Upper":18446744073709551616}',                # overflow rejected
+    ]
+    out = run(["json"], "\n".join(lines) + "\n").stdout.splitlines()
+    assert out[0] == lines[0] + "\t[Request bradfitz 0 9999]"
+    assert out[1] == '{"Type":2,"Data":"","Lower":0,"Upper":0,"Hash":18446744073709551615,"Nonce":5}' \
+                     "\t[Result 18446744073709551615 5]"
+    assert out[2].split("\t")[0] == \
+        '{"Type":1,"Data":"a\\u003cb\\u003e\\u0026\\"c\\\\ é\\u0001\\n","Lower":1,"Upper":2,"Hash":0,"Nonce":0}'
+    assert out[3] == '{"Type":0,"Data":"","Lower":0,"Upper":0,"Hash":0,"Nonce":0}\t[Join]'
+    assert out[4] == "ERROR" and out[5] == "ERROR"
+    # what Python's json makes of our bytes is the same message back
+    assert json.loads(out[2].split("\t")[0])["Data"] == 'a<b>&"c\\ é\u0001\n'
+
+
+def test_cli_usage_errors():
+    assert run([]).returncode == 2
+    assert run(["scan", "x", "1"]).returncode == 2
+    assert run(["scan", "x", "-1", "5"]).returncode == 2
+
+
+@pytest.mark.gpu
+def test_cli_scan_config1():
+    # configs[0]: "client 'bradfitz' maxNonce 9999" prints this line (client.go:59-61)
+    r = run(["scan", "bradfitz", "0", "9999"])
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "Result 1419516646206828 9898"
+    r = run(["hash", "msg", "1"])
+    assert r.stdout.strip() == "4754799531757243342"
+
+
+@pytest.mark.gpu
+def test_cli_serve_loop(oracle_mod):
+    reqs = [
+        {"Type": 0, "Data": "", "Lower": 0, "Upper": 0, "Hash": 0, "Nonce": 0},    # Join: ignored
+        {"Type": 1, "Data": "bradfitz", "Lower": 0, "Upper": 9999, "Hash": 0, "Nonce": 0},
+        {"Type": 1, "Data": "msg", "Lower": 0, "Upper": 2, "Hash": 0, "Nonce": 0},
+        {"Type": 1, "Data": "héllo", "Lower": 10**9 - 3000, "Upper": 10**9 + 3000, "Hash": 0, "Nonce": 0},
+        {"Type": 1, "Data": "x", "Lower": 9, "Upper": 3, "Hash": 0, "Nonce": 0},
+    ]
+    stdin = "\n".join(json.dumps(r, ensure_ascii=False) for r in reqs) + "\n"
+    r = run(["serve", "--device", "0", "--chunk", "1000"], stdin)  # small chunks: exercises chunking
+    assert r.returncode == 0, r.stderr
+    res = [json.loads(x) for x in r.stdout.splitlines()]
+    assert len(res) == 4 and all(x["Type"] == 2 for x in res)
+    want = [oracle_mod.scan(q["Data"], q["Lower"], q["Upper"], threads=8) for q in reqs[1:]]
+    assert [(x["Hash"], x["Nonce"]) for x in res] == want
+    assert want[-1] == (U64_MAX, 0)

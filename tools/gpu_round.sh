@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU-box session: VALU micro-benchmark, GPU parity tests, bench, rocprof.
+# One GPU-box session: VALU micro-benchmark, GPU parity tests, smoke, bench,
+# rocprofv3 kernel-trace stats and PMC counter passes.
 # Each GPU step has its own time limit.  A test FAILURE (exit 1) does not stop
 # the session; any fault/abort/timeout (other non-zero codes) ends it at once.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
@@ -16,12 +17,24 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-[ "${SKIP_PEAK:-0}" = 1 ] || step valu_peak 120 "$ROOT/tools/valu_peak" > "$OUT/${TAG}_valu_peak.jsonl"
+[ "${SKIP_PEAK:-0}" = 1 ] || step valu_peak 300 "$ROOT/tools/valu_peak" > "$OUT/${TAG}_valu_peak.jsonl"
 [ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest "$ROOT/tests" -m gpu -x -q -p no:cacheprovider > "$OUT/${TAG}_pytest_gpu.log" 2>&1
 [ "${SKIP_SMOKE:-0}" = 1 ] || step smoke 300 python -c "import sys; sys.path.insert(0, '$ROOT'); import __graft_entry__ as g; g.smoke()" > "$OUT/${TAG}_smoke.log" 2>&1
-step bench 600 python "$ROOT/bench.py" ${BENCH_ARGS:-} > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
+[ "${SKIP_BENCH:-0}" = 1 ] || step bench 600 python "$ROOT/bench.py" ${BENCH_ARGS:-} > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
+[ -z "${EXTRA_BENCH:-}" ] || step bench_extra 600 python "$ROOT/bench.py" $EXTRA_BENCH > "$OUT/${TAG}_bench_extra.json" 2> "$OUT/${TAG}_bench_extra.err"
+for lib in ${VARIANTS:-}; do
+  n=$(basename "$lib" .so)
+  P1HIP_LIB="$ROOT/$lib" step "bench_$n" 600 python "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu > "$OUT/${TAG}_bench_$n.json" 2> "$OUT/${TAG}_bench_$n.err"
+done
+cd /tmp && export TMPDIR=/tmp
 if [ "${SKIP_PROF:-0}" != 1 ]; then
-  cd /tmp && export TMPDIR=/tmp
   step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu
+fi
+if [ "${SKIP_PMC:-0}" != 1 ]; then
+  i=0
+  for set in "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i+1))
+    step pmc$i 600 rocprofv3 --pmc $set --kernel-include-regex k_scan_fast -d "$OUT/${TAG}_pmc$i" -o pmc --output-format csv -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu
+  done
 fi
 echo "== done"

@@ -14,43 +14,46 @@ constexpr int kIters = 4096;
 constexpr int kChains = 8;   // independent dependency chains per lane
 constexpr int kPerIter = 4;  // instructions per chain per iteration
 
+#define P1_BODY4(I) asm volatile(I "\n\t" I "\n\t" I "\n\t" I : "+v"(r[c]) : "v"(s1), "v"(s2))
+
 template <int OP>
 __global__ __launch_bounds__(256) void k_valu(uint32_t* out, uint32_t seed) {
   uint32_t r[kChains];
 #pragma unroll
   for (int c = 0; c < kChains; ++c) r[c] = seed * (threadIdx.x + 1) + c;
-  const uint32_t s1 = seed ^ 0x9e3779b9u, s2 = seed + 7u;
+  const uint32_t s1 = seed ^ 0x9e3779b9u, s2 = (seed + 7u) & 31u;
   for (int it = 0; it < kIters; ++it) {
 #pragma unroll
     for (int c = 0; c < kChains; ++c) {
-      if (OP == 0) {
-        asm volatile(
-            "v_alignbit_b32 %0, %0, %0, 7\n\t"
-            "v_alignbit_b32 %0, %0, %0, 13\n\t"
-            "v_alignbit_b32 %0, %0, %0, 5\n\t"
-            "v_alignbit_b32 %0, %0, %0, 11"
-            : "+v"(r[c]));
-      } else if (OP == 1) {
-        asm volatile(
-            "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\t"
-            "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca\n\t"
-            "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8\n\t"
-            "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96"
-            : "+v"(r[c]) : "v"(s1), "v"(s2));
-      } else if (OP == 2) {
-        asm volatile(
-            "v_add3_u32 %0, %0, %1, %2\n\t"
-            "v_add3_u32 %0, %0, %1, %2\n\t"
-            "v_add3_u32 %0, %0, %1, %2\n\t"
-            "v_add3_u32 %0, %0, %1, %2"
-            : "+v"(r[c]) : "v"(s1), "v"(s2));
-      } else {
-        asm volatile(
-            "v_add_u32_e32 %0, %0, %1\n\t"
-            "v_xor_b32_e32 %0, %0, %2\n\t"
-            "v_add_u32_e32 %0, %0, %1\n\t"
-            "v_xor_b32_e32 %0, %0, %2"
-            : "+v"(r[c]) : "v"(s1), "v"(s2));
+      if (OP == 0) P1_BODY4("v_alignbit_b32 %0, %0, %0, 7");
+      else if (OP == 1) P1_BODY4("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96");
+      else if (OP == 2) P1_BODY4("v_add3_u32 %0, %0, %1, %2");
+      else if (OP == 3) P1_BODY4("v_add_u32_e32 %0, %0, %1");
+      else if (OP == 4) P1_BODY4("v_xor_b32_e32 %0, %0, %1");
+      else if (OP == 5) P1_BODY4("v_lshrrev_b32_e32 %0, 7, %0");
+      else if (OP == 6) P1_BODY4("v_lshl_or_b32 %0, %0, 7, %1");
+      else if (OP == 7) P1_BODY4("v_alignbyte_b32 %0, %0, %1, 1");
+      else if (OP == 8) P1_BODY4("v_perm_b32 %0, %0, %1, %2");
+      else if (OP == 9) P1_BODY4("v_xad_u32 %0, %0, %1, %2");
+      else if (OP == 10) P1_BODY4("v_or3_b32 %0, %0, %1, %2");
+      else if (OP == 11) P1_BODY4("v_lshl_add_u32 %0, %0, 3, %1");
+      else if (OP == 12) P1_BODY4("v_add_lshl_u32 %0, %0, %1, 3");
+      else if (OP == 13) P1_BODY4("v_and_or_b32 %0, %0, %1, %2");
+      else if (OP == 14) P1_BODY4("v_bfi_b32 %0, %0, %1, %2");
+      else if (OP == 15) P1_BODY4("v_add_u32_e64 %0, %0, %1");
+      else if (OP == 16) P1_BODY4("v_lshrrev_b32_e64 %0, %2, %0");
+      else if (OP == 17) P1_BODY4("v_alignbit_b32 %0, %0, %1, %2");
+      else if (OP == 18) P1_BODY4("v_pk_add_u16 %0, %0, %1");
+      else if (OP == 19) P1_BODY4("v_bfe_u32 %0, %0, 3, 20");
+      else if (OP == 20) P1_BODY4("v_mad_u32_u24 %0, %0, %1, %2");
+      else if (OP == 21) P1_BODY4("v_cndmask_b32_e64 %0, %0, %1, s[0:1]");
+      else if (OP == 22) P1_BODY4("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca");
+      else if (OP == 23) P1_BODY4("v_bitop3_b16 %0, %0, %1, %2 bitop3:0x96");
+      else if (OP == 24) P1_BODY4("v_mov_b32_e32 %0, %1");
+      else if (OP == 25) {  // half alignbit, half bitop3 interleaved
+        asm volatile("v_alignbit_b32 %0, %0, %0, 7\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\t"
+                     "v_alignbit_b32 %0, %0, %0, 9\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0xca"
+                     : "+v"(r[c]) : "v"(s1), "v"(s2));
       }
     }
   }
@@ -67,7 +70,7 @@ static int run(const char* name, int cus) {
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
-  for (int wps : {1, 2, 4, 8}) {
+  for (int wps : {2, 8}) {
     // blocks of 256 threads = 4 waves = one wave per SIMD; wps blocks per CU
     const int blocks = cus * wps;  // one round: wps waves on every SIMD
     hipLaunchKernelGGL(k_valu<OP>, dim3(blocks), dim3(256), 0, 0, d, 1u);
@@ -92,9 +95,14 @@ int main() {
   CHK(hipGetDeviceProperties(&p, 0));
   printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d}\n", p.gcnArchName, p.multiProcessorCount, p.clockRate);
   int cus = p.multiProcessorCount;
-  if (run<0>("v_alignbit_b32", cus)) return 1;
-  if (run<1>("v_bitop3_b32", cus)) return 1;
-  if (run<2>("v_add3_u32", cus)) return 1;
-  if (run<3>("v_add_u32+v_xor_b32", cus)) return 1;
+#define RUN(I, N) if (run<I>(N, cus)) return 1
+  RUN(0, "v_alignbit_b32 (x,x,imm)"); RUN(17, "v_alignbit_b32 (x,y,vgpr)"); RUN(7, "v_alignbyte_b32");
+  RUN(1, "v_bitop3_b32 0x96"); RUN(22, "v_bitop3_b32 0xca"); RUN(23, "v_bitop3_b16");
+  RUN(2, "v_add3_u32"); RUN(3, "v_add_u32_e32"); RUN(15, "v_add_u32_e64"); RUN(4, "v_xor_b32_e32");
+  RUN(5, "v_lshrrev_b32_e32"); RUN(16, "v_lshrrev_b32_e64"); RUN(6, "v_lshl_or_b32"); RUN(8, "v_perm_b32");
+  RUN(9, "v_xad_u32"); RUN(10, "v_or3_b32"); RUN(11, "v_lshl_add_u32"); RUN(12, "v_add_lshl_u32");
+  RUN(13, "v_and_or_b32"); RUN(14, "v_bfi_b32"); RUN(18, "v_pk_add_u16"); RUN(19, "v_bfe_u32");
+  RUN(20, "v_mad_u32_u24"); RUN(21, "v_cndmask_b32_e64"); RUN(24, "v_mov_b32"); RUN(25, "alignbit/bitop3 mix");
+#undef RUN
   return 0;
 }
