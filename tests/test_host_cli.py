@@ -28,21 +28,21 @@ def test_json_wire_format_matches_go():
     lines = [
         '{"Type":1,"Data":"bradfitz","Lower":0,"Upper":9999,"Hash":0,"Nonce":0}',
         '{"type":2,"hash":18446744073709551615,"nonce":5}',       # Go matches keys case-insensitively
-        '{"Type":1,"Data":"a<b>&\\"c\\\\ \\u00e9\\u0001\\n","Lower":1,"Upper":2}',
+        '{"Type":1,"Data":"a<b>&\\"c\\\\ \\u00e9\\u0001\\u2028","Lower":1,"Upper":2}',
         '{"Type":0,"Extra":[1,{"x":null}],"Data":null}',          # unknown keys / null ignored
         '{"Type":1,"Lower":-1}',                                  # negative uint64 rejected
         '{"Type":1,"Upper":18446744073709551616}',                # overflow rejected
     ]
-    out = run(["json"], "\n".join(lines) + "\n").stdout.splitlines()
+    out = run(["json"], "\n".join(lines) + "\n").stdout.split("\n")
     assert out[0] == lines[0] + "\t[Request bradfitz 0 9999]"
     assert out[1] == '{"Type":2,"Data":"","Lower":0,"Upper":0,"Hash":18446744073709551615,"Nonce":5}' \
                      "\t[Result 18446744073709551615 5]"
     assert out[2].split("\t")[0] == \
-        '{"Type":1,"Data":"a\\u003cb\\u003e\\u0026\\"c\\\\ é\\u0001\\n","Lower":1,"Upper":2,"Hash":0,"Nonce":0}'
+        '{"Type":1,"Data":"a\\u003cb\\u003e\\u0026\\"c\\\\ é\\u0001\\u2028","Lower":1,"Upper":2,"Hash":0,"Nonce":0}'
     assert out[3] == '{"Type":0,"Data":"","Lower":0,"Upper":0,"Hash":0,"Nonce":0}\t[Join]'
     assert out[4] == "ERROR" and out[5] == "ERROR"
     # what Python's json makes of our bytes is the same message back
-    assert json.loads(out[2].split("\t")[0])["Data"] == 'a<b>&"c\\ é\u0001\n'
+    assert json.loads(out[2].split("\t")[0])["Data"] == 'a<b>&"c\\ é\u0001\u2028'
 
 
 def test_cli_usage_errors():
