@@ -79,23 +79,22 @@ int p1hip_hash(const uint8_t *msg, size_t msg_len, uint64_t nonce, uint64_t *out
 int p1hip_reduce_pairs(const uint64_t *hashes, const uint64_t *nonces, size_t n,
                        uint64_t *out_hash, uint64_t *out_nonce);
 
-/* Kernel-level accounting for the dominant (fast scan) kernel. */
+/* Kernel-level accounting.  One p1hip_scan = one (rarely several) launch of
+ * the scan kernel k_scan per device, covering every decade of the range. */
 typedef struct {
-  uint64_t scans;           /* p1hip_scan calls since reset                       */
-  uint64_t fast_launches;   /* launches of the fast scan kernel                   */
-  uint64_t fast_nonces;     /* nonces hashed by those launches                    */
-  uint64_t fast_alg_ops;    /* algorithmic int32 ops: 1384 * B_tail per nonce     */
-  double fast_kernel_ms;    /* sum of HIP-event durations of those launches
-                               (only while profiling is on, else 0); launches
-                               of one scan may overlap on the device's streams  */
-  uint64_t generic_launches;/* launches of the generic (edge) kernel              */
-  uint64_t generic_nonces;  /* nonces hashed by the generic kernel                */
-  double scan_wall_ms;      /* host wall time inside p1hip_scan                   */
-  /* the largest fast launch of each scan ("dominant kernel" for the roofline) */
-  uint64_t dom_launches;
-  uint64_t dom_nonces;
-  uint64_t dom_alg_ops;
-  double dom_kernel_ms;     /* HIP-event durations (profiling on)                 */
+  uint64_t scans;            /* p1hip_scan calls since reset                      */
+  uint64_t fast_launches;    /* fast segments (one thread per 10^k nonces)        */
+  uint64_t fast_nonces;      /* nonces hashed by fast segments                    */
+  uint64_t fast_alg_ops;     /* algorithmic int32 ops: 1384 * B_tail per nonce    */
+  double fast_kernel_ms;     /* unused (0), kept for layout stability             */
+  uint64_t generic_launches; /* generic segments (one thread per nonce)           */
+  uint64_t generic_nonces;   /* nonces hashed by generic segments                 */
+  double scan_wall_ms;       /* host wall time inside p1hip_scan                  */
+  uint64_t scan_launches;    /* launches of k_scan                                */
+  uint64_t scan_nonces;      /* nonces hashed by those launches                   */
+  uint64_t scan_alg_ops;     /* their algorithmic int32 ops (1384 * B_tail each)  */
+  double scan_kernel_ms;     /* sum of HIP-event durations of those launches
+                                (recorded only while profiling is on)            */
 } p1hip_stats_t;
 
 /* Record HIP events (on the library's own stream) around every fast-kernel

@@ -28,10 +28,10 @@ class Stats(ctypes.Structure):
         ("generic_launches", U64),
         ("generic_nonces", U64),
         ("scan_wall_ms", ctypes.c_double),
-        ("dom_launches", U64),
-        ("dom_nonces", U64),
-        ("dom_alg_ops", U64),
-        ("dom_kernel_ms", ctypes.c_double),
+        ("scan_launches", U64),
+        ("scan_nonces", U64),
+        ("scan_alg_ops", U64),
+        ("scan_kernel_ms", ctypes.c_double),
     ]
 
     def as_dict(self):

@@ -5,9 +5,11 @@
 // miner/miner.go:56-63 (see include/p1hip.h for the exact contract).
 //
 // Device pipeline of one p1hip_scan on one device (one HIP stream):
-//   planner.hpp  -> list of launches (fast: one thread per 10^k nonces;
+//   planner.hpp  -> list of pieces (fast: one thread per 10^k nonces;
 //                   generic: one thread per nonce, for ragged edges)
-//   k_scan_fast<FV,NV,TRAIL> / k_scan_generic
+//   k_scan       -> one launch, one segment per piece (variant chosen per
+//                   workgroup from the segment table: fast_thread<FV,NV,TRAIL>
+//                   or generic_thread)
 //                -> per-thread best (hash, nonce) -> wave argmin with DPP
 //                   (quad_perm, row_ror) + ds_swizzle + readlane -> LDS across
 //                   the 4 waves -> one 16-byte partial per workgroup
@@ -16,6 +18,8 @@
 // all-gather of the 16-byte results (ncclCommInitAll), host lexicographic min.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+
+#include <string.h>
 
 #include <algorithm>
 #include <chrono>
@@ -95,18 +99,50 @@ __device__ __forceinline__ void block_min_store(Key k, Key* out) {
 // Minimum waves per SIMD the register allocator must leave room for
 // (tuned on MI355X); override with -DP1_FAST_WAVES=n.
 #ifndef P1_FAST_WAVES
-#define P1_FAST_WAVES 5
+#define P1_FAST_WAVES 4
 #endif
 
-template <int FV, int NV, bool TRAIL>
-__global__ __launch_bounds__(kBlock, P1_FAST_WAVES) void k_scan_fast(const FastArgs A, Key* __restrict__ part) {
-  const Key k = fast_thread<FV, NV, TRAIL>(A, blockIdx.x * kBlock + threadIdx.x);
-  block_min_store<kBlock>(k, part + A.part_off + blockIdx.x);
+// Variant id of a fast segment; kGenericKind marks a generic segment.
+__host__ __device__ constexpr uint32_t variant_id(int fv, int nv, bool trail) {
+  return (trail ? 64u : 0u) + (uint32_t)fv * 2u + (uint32_t)(nv - 1);
 }
+constexpr uint32_t kGenericKind = 255;
 
-__global__ __launch_bounds__(kBlock) void k_scan_generic(const GenArgs A, Key* __restrict__ part) {
-  const Key k = generic_thread(A, (uint64_t)blockIdx.x * kBlock + threadIdx.x);
-  block_min_store<kBlock>(k, part + A.part_off + blockIdx.x);
+// One segment of a scan launch: a contiguous run of workgroups that all do
+// the same kind of work (one decade piece).
+struct Segment {
+  uint32_t kind;    // variant_id(...) or kGenericKind
+  uint32_t block0;  // first workgroup of the segment within the launch
+  uint32_t pad[2];
+  FastArgs fa;
+  GenArgs ga;
+};
+
+// The scan kernel: every workgroup finds its segment (wave-uniform scalar
+// loop over the table), runs that segment's per-thread work and writes one
+// 16-byte partial.  All decades of a scan -- and their ragged edges -- share
+// one launch, so there is one grid drain per scan, filled by the short
+// segments that are placed last.
+__global__ __launch_bounds__(kBlock, P1_FAST_WAVES) void k_scan(const Segment* __restrict__ segs, uint32_t nseg,
+                                                                Key* __restrict__ part) {
+  const uint32_t b = blockIdx.x;
+  uint32_t si = 0;
+  while (si + 1 < nseg && segs[si + 1].block0 <= b) ++si;
+  const Segment& S = segs[si];
+  const uint32_t local = (b - S.block0) * kBlock + threadIdx.x;
+  Key k;
+  switch (S.kind) {
+#define P1_CASE(FV, NV, TR)                         \
+  case variant_id(FV, NV, TR):                      \
+    k = fast_thread<FV, NV, TR>(S.fa, local);       \
+    break;
+#include "fast_variants.inc"
+#undef P1_CASE
+    default:
+      k = generic_thread(S.ga, local);
+      break;
+  }
+  block_min_store<kBlock>(k, part + b);
 }
 
 constexpr int kReduceThreads = 1024;
@@ -127,14 +163,12 @@ __global__ __launch_bounds__(kBlock) void k_pairs(const uint64_t* __restrict__ h
   block_min_store<kBlock>(k, part + blockIdx.x);
 }
 
-typedef void (*FastKernel)(const FastArgs, Key*);
-
-static FastKernel fast_kernel(int fv, int nv, bool trail) {
+static bool has_variant(int fv, int nv, bool trail) {
 #define P1_CASE(FV, NV, TR) \
-  if (fv == FV && nv == NV && trail == TR) return &k_scan_fast<FV, NV, TR>;
+  if (fv == FV && nv == NV && trail == TR) return true;
 #include "fast_variants.inc"
 #undef P1_CASE
-  return nullptr;
+  return false;
 }
 
 // ----------------------------------------------------------------------------
@@ -163,29 +197,27 @@ int fail(int rc, const std::string& what) {
       return fail(P1HIP_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_));      \
   } while (0)
 
-// Launches of one scan are spread over kStreams streams (largest first) so
-// that the drain of one decade's grid overlaps the next one's work; the
-// reduction waits for all of them on the main stream.
-constexpr int kStreams = 4;
+constexpr uint32_t kMaxSegs = 64;              // segments per launch
+constexpr uint32_t kMaxLaunchBlocks = 1u << 20;  // workgroups per launch
 
 struct Dev {
   int ordinal = -1;
-  hipStream_t stream = nullptr;            // main stream (= streams[0])
-  hipStream_t aux[kStreams - 1] = {};      // streams[1..]
-  hipEvent_t join[kStreams - 1] = {};      // aux -> main dependencies
+  hipStream_t stream = nullptr;
   Key* d_part = nullptr;
   size_t part_cap = 0;
-  Key* d_res = nullptr;     // 1 Key
-  Key* d_gather = nullptr;  // ndev Keys (multi-device)
-  Key* h_res = nullptr;     // pinned, ndev Keys
+  Key* d_res = nullptr;         // 1 Key
+  Key* d_gather = nullptr;      // ndev Keys (multi-device)
+  Key* h_res = nullptr;         // pinned, ndev Keys
+  Segment* d_seg = nullptr;     // segment tables, kMaxSegs per launch slot
+  Segment* h_seg = nullptr;     // pinned staging for the tables
+  size_t seg_cap = 0;           // launch slots allocated
   ncclComm_t comm = nullptr;
   std::vector<hipEvent_t> evs;  // profiling event pool (pairs)
-  // per-scan accounting filled by run_plan
+  // per-scan accounting filled by run_range
   uint64_t fast_launches = 0, fast_nonces = 0, fast_ops = 0, gen_launches = 0, gen_nonces = 0;
   double fast_ms = 0.0;
-  uint64_t dom_nonces = 0, dom_ops = 0;  // largest fast launch of the scan
-  double dom_ms = 0.0;
-  hipStream_t pick(int i) const { return i == 0 ? stream : aux[i - 1]; }
+  uint64_t scan_launches = 0, scan_nonces = 0, scan_ops = 0;
+  double scan_ms = 0.0;
 };
 
 struct Runtime {
@@ -206,10 +238,8 @@ int dev_release(Dev& d) {
   if (d.stream) (void)hipStreamSynchronize(d.stream);
   for (hipEvent_t e : d.evs) (void)hipEventDestroy(e);
   d.evs.clear();
-  for (int i = 0; i < kStreams - 1; ++i) {
-    if (d.join[i]) (void)hipEventDestroy(d.join[i]);
-    if (d.aux[i]) (void)hipStreamDestroy(d.aux[i]);
-  }
+  if (d.d_seg) (void)hipFree(d.d_seg);
+  if (d.h_seg) (void)hipHostFree(d.h_seg);
   if (d.comm) ncclCommDestroy(d.comm);
   if (d.d_part) (void)hipFree(d.d_part);
   if (d.d_res) (void)hipFree(d.d_res);
@@ -249,10 +279,6 @@ int init_locked(Runtime& R, const std::vector<int>& ords) {
     d.ordinal = ords[i];
     HIPCHK(hipSetDevice(d.ordinal));
     HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    for (int j = 0; j < kStreams - 1; ++j) {
-      HIPCHK(hipStreamCreateWithFlags(&d.aux[j], hipStreamNonBlocking));
-      HIPCHK(hipEventCreateWithFlags(&d.join[j], hipEventDisableTiming));
-    }
     HIPCHK(hipMalloc(&d.d_res, sizeof(Key)));
     HIPCHK(hipMalloc(&d.d_gather, sizeof(Key) * nd));
     HIPCHK(hipHostMalloc(&d.h_res, sizeof(Key) * nd, hipHostMallocDefault));
@@ -279,80 +305,111 @@ int ensure_init(Runtime& R) {
 int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, bool profiling) {
   HIPCHK(hipSetDevice(d.ordinal));
   d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
-  d.dom_nonces = d.dom_ops = 0;
-  d.fast_ms = d.dom_ms = 0.0;
+  d.scan_launches = d.scan_nonces = d.scan_ops = 0;
+  d.fast_ms = d.scan_ms = 0.0;
   Plan plan;
   std::string err = make_plan(msg, len, lo, hi, plan);
   if (!err.empty()) return fail(P1HIP_ERR_ARGS, "planner: " + err);
-  if (plan.total_blocks > d.part_cap) {
+  // Longest-running workgroups first: fast pieces by lo-loop length (10^k),
+  // then generic pieces, so short work fills the grid's drain.
+  std::vector<size_t> order(plan.launches.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+  auto weight = [&](size_t i) -> uint64_t {
+    const Launch& L = plan.launches[i];
+    return L.fast ? (uint64_t)L.fa.kpow * (uint64_t)L.btail : (uint64_t)L.btail - 1;
+  };
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return weight(a) > weight(b); });
+  // pack into launches of <= kMaxSegs segments / kMaxLaunchBlocks workgroups
+  struct Batch { size_t first, count; uint32_t blocks; };
+  std::vector<Batch> batches;
+  uint32_t total_blocks = 0;
+  for (size_t r = 0; r < order.size(); ++r) {
+    const Launch& L = plan.launches[order[r]];
+    if (batches.empty() || batches.back().count == kMaxSegs ||
+        batches.back().blocks + (uint64_t)L.blocks > kMaxLaunchBlocks)
+      batches.push_back({r, 0, 0});
+    batches.back().count++;
+    batches.back().blocks += L.blocks;
+    total_blocks += L.blocks;
+  }
+  if (total_blocks > d.part_cap) {
     if (d.d_part) HIPCHK(hipFree(d.d_part));
     d.d_part = nullptr;
     size_t cap = 1;
-    while (cap < plan.total_blocks) cap <<= 1;
+    while (cap < total_blocks) cap <<= 1;
     HIPCHK(hipMalloc(&d.d_part, cap * sizeof(Key)));
     d.part_cap = cap;
   }
-  // largest launches first, dealt round-robin over the streams
-  std::vector<size_t> order(plan.launches.size());
-  for (size_t i = 0; i < order.size(); ++i) order[i] = i;
-  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
-    return plan.launches[a].nonces * plan.launches[a].btail > plan.launches[b].nonces * plan.launches[b].btail;
-  });
-  const size_t dom = order.empty() ? 0 : order[0];
-  std::vector<size_t> ev_launch;  // launch index of each timed event pair
+  if (batches.size() > d.seg_cap) {
+    if (d.d_seg) HIPCHK(hipFree(d.d_seg));
+    if (d.h_seg) HIPCHK(hipHostFree(d.h_seg));
+    d.d_seg = nullptr;
+    d.h_seg = nullptr;
+    size_t cap = 4;
+    while (cap < batches.size()) cap <<= 1;
+    HIPCHK(hipMalloc(&d.d_seg, cap * kMaxSegs * sizeof(Segment)));
+    HIPCHK(hipHostMalloc(&d.h_seg, cap * kMaxSegs * sizeof(Segment), hipHostMallocDefault));
+    d.seg_cap = cap;
+  }
   size_t nev = 0;
-  int used = 1;
-  for (size_t r = 0; r < order.size(); ++r) {
-    const Launch& L = plan.launches[order[r]];
-    const int si = (int)(r % kStreams);
-    hipStream_t st = d.pick(si);
-    if (si + 1 > used) used = si + 1;
-    if (L.fast) {
-      FastKernel fn = fast_kernel(L.fv, L.nv, L.trail);
-      if (!fn) return fail(P1HIP_ERR_ARGS, "no fast kernel variant");
-      if (profiling) {
-        while (d.evs.size() < nev + 2) {
-          hipEvent_t e;
-          HIPCHK(hipEventCreate(&e));
-          d.evs.push_back(e);
-        }
-        HIPCHK(hipEventRecord(d.evs[nev], st));
+  uint32_t part_off = 0;
+  for (size_t bi = 0; bi < batches.size(); ++bi) {
+    const Batch& B = batches[bi];
+    Segment* hs = d.h_seg + bi * kMaxSegs;
+    uint64_t ops = 0, nonces = 0;
+    uint32_t block0 = 0;
+    for (size_t j = 0; j < B.count; ++j) {
+      const Launch& L = plan.launches[order[B.first + j]];
+      Segment& S = hs[j];
+      memset(&S, 0, sizeof S);
+      S.block0 = block0;
+      block0 += L.blocks;
+      if (L.fast) {
+        if (!has_variant(L.fv, L.nv, L.trail)) return fail(P1HIP_ERR_ARGS, "no fast kernel variant");
+        S.kind = variant_id(L.fv, L.nv, L.trail);
+        S.fa = L.fa;
+        d.fast_launches++;
+        d.fast_nonces += L.nonces;
+        d.fast_ops += L.nonces * kAlgOpsPerCompression * (uint64_t)L.btail;
+      } else {
+        S.kind = kGenericKind;
+        S.ga = L.ga;
+        d.gen_launches++;
+        d.gen_nonces += L.nonces;
       }
-      hipLaunchKernelGGL(fn, dim3(L.blocks), dim3(kBlock), 0, st, L.fa, d.d_part);
-      HIPCHK(hipGetLastError());
-      if (profiling) {
-        HIPCHK(hipEventRecord(d.evs[nev + 1], st));
-        ev_launch.push_back(order[r]);
-        nev += 2;
-      }
-      d.fast_launches++;
-      d.fast_nonces += L.nonces;
-      d.fast_ops += L.nonces * kAlgOpsPerCompression * (uint64_t)L.btail;
-      if (order[r] == dom) {
-        d.dom_nonces += L.nonces;
-        d.dom_ops += L.nonces * kAlgOpsPerCompression * (uint64_t)L.btail;
-      }
-    } else {
-      hipLaunchKernelGGL(k_scan_generic, dim3(L.blocks), dim3(kBlock), 0, st, L.ga, d.d_part);
-      HIPCHK(hipGetLastError());
-      d.gen_launches++;
-      d.gen_nonces += L.nonces;
+      nonces += L.nonces;
+      ops += L.nonces * kAlgOpsPerCompression * (uint64_t)L.btail;
     }
+    Segment* ds = d.d_seg + bi * kMaxSegs;
+    HIPCHK(hipMemcpyAsync(ds, hs, B.count * sizeof(Segment), hipMemcpyHostToDevice, d.stream));
+    if (profiling) {
+      while (d.evs.size() < nev + 2) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        d.evs.push_back(e);
+      }
+      HIPCHK(hipEventRecord(d.evs[nev], d.stream));
+    }
+    hipLaunchKernelGGL(k_scan, dim3(B.blocks), dim3(kBlock), 0, d.stream, ds, (uint32_t)B.count,
+                       d.d_part + part_off);
+    HIPCHK(hipGetLastError());
+    if (profiling) {
+      HIPCHK(hipEventRecord(d.evs[nev + 1], d.stream));
+      nev += 2;
+    }
+    part_off += B.blocks;
+    d.scan_launches++;
+    d.scan_nonces += nonces;
+    d.scan_ops += ops;
   }
-  for (int j = 1; j < used; ++j) {
-    HIPCHK(hipEventRecord(d.join[j - 1], d.aux[j - 1]));
-    HIPCHK(hipStreamWaitEvent(d.stream, d.join[j - 1], 0));
-  }
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, d.stream, d.d_part, plan.total_blocks,
-                     d.d_res);
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, d.stream, d.d_part, total_blocks, d.d_res);
   HIPCHK(hipGetLastError());
   if (profiling && nev) {
+    HIPCHK(hipEventSynchronize(d.evs[nev - 1]));
     for (size_t i = 0; i < nev; i += 2) {
-      HIPCHK(hipEventSynchronize(d.evs[i + 1]));
       float ms = 0.f;
       HIPCHK(hipEventElapsedTime(&ms, d.evs[i], d.evs[i + 1]));
-      d.fast_ms += ms;
-      if (ev_launch[i / 2] == dom) d.dom_ms += ms;
+      d.scan_ms += ms;
     }
   }
   return P1HIP_OK;
@@ -473,10 +530,10 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
       R.stats.fast_kernel_ms += d.fast_ms;
       R.stats.generic_launches += d.gen_launches;
       R.stats.generic_nonces += d.gen_nonces;
-      if (d.dom_nonces) R.stats.dom_launches++;
-      R.stats.dom_nonces += d.dom_nonces;
-      R.stats.dom_alg_ops += d.dom_ops;
-      R.stats.dom_kernel_ms += d.dom_ms;
+      R.stats.scan_launches += d.scan_launches;
+      R.stats.scan_nonces += d.scan_nonces;
+      R.stats.scan_alg_ops += d.scan_ops;
+      R.stats.scan_kernel_ms += d.scan_ms;
     }
   }
   R.stats.scans++;

@@ -10,9 +10,11 @@
 //      tail layout (which bytes hold which digit, B_tail, the bit length) is
 //      uniform per launch;
 //   2. inside a decade, nonce = hi * 10^k + lo.  Whole 10^k-aligned blocks go
-//      to the fast kernel (one thread per hi value, at most kMaxFastThreads
-//      per launch); the ragged edges and decades with d <= k go to the
-//      generic kernel (one thread per nonce).
+//      to a fast piece (one thread per hi value, at most kMaxFastThreads per
+//      piece); the ragged edges and decades with d <= k go to generic pieces
+//      (one thread per nonce).
+//   3. the pieces become the segments of one multi-segment k_scan launch
+//      (p1hip.hip), longest-running workgroups first.
 // k is 3 except where the last 3 digits would straddle the two tail blocks;
 // then k = 1 or 2 so that all lo digits sit in the last block.
 #pragma once
@@ -26,8 +28,8 @@
 
 namespace p1 {
 
-constexpr uint64_t kMaxFastThreads = 1ull << 24;   // hi values per fast launch
-constexpr uint64_t kMaxGenericThreads = 1ull << 24; // nonces per generic launch
+constexpr uint64_t kMaxFastThreads = 1ull << 26;   // hi values per fast piece
+constexpr uint64_t kMaxGenericThreads = 1ull << 26; // nonces per generic piece
 constexpr uint64_t kAlgOpsPerCompression = 1384;
 // A fast launch wants >= 4 waves on each of the 1024 SIMDs; decades too small
 // for that at k = 3 drop to k = 2 or 1 (shorter per-thread loops, more threads)

@@ -127,7 +127,7 @@ P1_HD void place_digits(const uint32_t* tmpl, uint64_t x, uint32_t ndig, uint32_
 P1_HD constexpr uint64_t var_mask(int fv, int nv) {
   uint64_t m = 0;
   for (int t = 0; t < 64; ++t) {
-    bool v;
+    bool v = false;
     if (t < 16) v = (t >= fv && t < fv + nv);
     else v = ((m >> (t - 2)) & 1) || ((m >> (t - 7)) & 1) || ((m >> (t - 15)) & 1) || ((m >> (t - 16)) & 1);
     if (v) m |= 1ull << t;

@@ -123,10 +123,11 @@ def test_stats_and_profiling(gpu):
     gpu.scan("bradfitz", 0, 10**8)
     s = gpu.get_stats()
     gpu.set_profiling(False)
-    assert s["scans"] == 1 and s["fast_launches"] >= 1
-    assert s["fast_nonces"] + s["generic_nonces"] == 10**8 + 1
-    assert s["fast_kernel_ms"] > 0
+    assert s["scans"] == 1 and s["fast_launches"] >= 1 and s["scan_launches"] == 1
+    assert s["fast_nonces"] + s["generic_nonces"] == 10**8 + 1 == s["scan_nonces"]
+    assert s["scan_kernel_ms"] > 0
     assert s["fast_alg_ops"] == 1384 * s["fast_nonces"]  # 'bradfitz' is 1 block per nonce
+    assert s["scan_alg_ops"] == 1384 * s["scan_nonces"]
 
 
 def test_init_variants(gpu):
