@@ -78,6 +78,9 @@ def main():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (production); gloo only to rehearse "
+                         "several ranks on one GPU")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -91,20 +94,26 @@ def main():
     import p1_amd
     from p1_amd.dist import distributed_scan
 
+    ngpu = torch.cuda.device_count()
+    gpu = local % ngpu if args.dist_backend == "gloo" else local  # gloo rehearsal may share a GPU
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    p1_amd.init_devices([local])
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    p1_amd.init_devices([gpu])
 
     msg = cfg["msg"]
     total = cfg["per_gpu"] * world
     shard = p1_amd.shard_range(0, total - 1, rank, world)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", gpu)
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     def step():
         if world == 1:
             return p1_amd.scan(msg, shard[0], shard[1])
-        return distributed_scan(msg, 0, total - 1, p1_amd.scan, device=dev)
+        return distributed_scan(msg, 0, total - 1, p1_amd.scan, device=coll_dev)
 
     def barrier():
         if world > 1:
@@ -124,7 +133,7 @@ def main():
     stats = p1_amd.get_stats()
 
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -172,7 +181,9 @@ def main():
                 "msg_len": len(msg),
                 "nonces_per_gpu": cfg["per_gpu"],
                 "job_range": [0, total - 1],
-                "parallelism": f"range-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+                "parallelism": f"range-shard x{world}" + (
+                    (" + RCCL all-gather" if args.dist_backend == "nccl" else " + gloo all-gather (rehearsal)")
+                    if world > 1 else ""),
             },
             "roofline": roofline,
             "result": {"hash": result[0], "nonce": result[1], "consistent": consistent,

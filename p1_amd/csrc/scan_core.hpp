@@ -156,16 +156,16 @@ P1_HD uint64_t fast_hash(const FastPre<FV, NV, TRAIL>& P, uint32_t wv0, uint32_t
   for (int t = 16; t < 64; ++t) {
     if (FP::var(t)) {
       uint32_t v = P.kw[t];
-      if (FP::var(t - 2)) v += ssig1(w[t - 2]);
-      if (FP::var(t - 7)) v += w[t - 7];
-      if (FP::var(t - 15)) v += ssig0(w[t - 15]);
-      if (FP::var(t - 16)) v += w[t - 16];
+      if (FP::var(t - 2)) v = add2(v, ssig1(w[t - 2]));
+      if (FP::var(t - 7)) v = add2(v, w[t - 7]);
+      if (FP::var(t - 15)) v = add2(v, ssig0(w[t - 15]));
+      if (FP::var(t - 16)) v = add2(v, w[t - 16]);
       w[t] = v;
     }
   }
   State s = P.s1;
-  s.v[0] += wv0;  // round FV, per-nonce half
-  s.v[4] += wv0;
+  s.v[0] = add2(s.v[0], wv0);  // round FV, per-nonce half
+  s.v[4] = add2(s.v[4], wv0);
 #pragma unroll
   for (int t = FV + 1; t < 64; ++t) sha_round(s, FP::var(t) ? k256(t) + w[t] : P.kw[t]);
   if constexpr (!TRAIL) {

@@ -98,6 +98,13 @@ P1_HD uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
   return (a & b) ^ (a & c) ^ (b & c);
 }
 
+// Two-input add.  Kept as a named helper: on gfx950 v_add3_u32 is a half-rate
+// op (tools/valu_peak), as is every other 3-operand VOP3 integer op except
+// v_bitop3_b32, but forcing plain v_add_u32 pairs costs the same issue cycles
+// and makes the compiler pad with s_nop (measured), so the
+// compiler's add3 fusion is left on.
+P1_HD uint32_t add2(uint32_t a, uint32_t b) { return a + b; }
+
 P1_HD uint32_t bsig0(uint32_t a) { return xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)); }
 P1_HD uint32_t bsig1(uint32_t e) { return xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)); }
 P1_HD uint32_t ssig0(uint32_t x) { return xor3(rotr(x, 7), rotr(x, 18), x >> 3); }
@@ -112,15 +119,15 @@ struct State {
 P1_HD void sha_round(State& s, uint32_t kw) {
   const uint32_t a = s.v[0], b = s.v[1], c = s.v[2], d = s.v[3];
   const uint32_t e = s.v[4], f = s.v[5], g = s.v[6], h = s.v[7];
-  const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kw;
-  const uint32_t t2 = bsig0(a) + maj(a, b, c);
-  s.v[7] = g; s.v[6] = f; s.v[5] = e; s.v[4] = d + t1;
-  s.v[3] = c; s.v[2] = b; s.v[1] = a; s.v[0] = t1 + t2;
+  const uint32_t t1 = add2(add2(add2(h, kw), bsig1(e)), ch(e, f, g));
+  const uint32_t t2 = add2(bsig0(a), maj(a, b, c));
+  s.v[7] = g; s.v[6] = f; s.v[5] = e; s.v[4] = add2(d, t1);
+  s.v[3] = c; s.v[2] = b; s.v[1] = a; s.v[0] = add2(t1, t2);
 }
 
 // Message-schedule word t >= 16 of a 64-entry array (unrolled callers only).
 P1_HD uint32_t sched(const uint32_t* w, int t) {
-  return ssig1(w[t - 2]) + w[t - 7] + ssig0(w[t - 15]) + w[t - 16];
+  return add2(add2(add2(ssig1(w[t - 2]), w[t - 7]), ssig0(w[t - 15])), w[t - 16]);
 }
 
 // Full compression of the block in w[0..15] chained into cv[8];

@@ -23,6 +23,10 @@ step() {  # step <name> <timeout> <cmd...>
 [ "${SKIP_SMOKE:-0}" = 1 ] || step smoke 300 python -c "import sys; sys.path.insert(0, '$ROOT'); import __graft_entry__ as g; g.smoke()" > "$OUT/${TAG}_smoke.log" 2>&1
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 600 python "$ROOT/bench.py" ${BENCH_ARGS:-} > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
 [ -z "${EXTRA_BENCH:-}" ] || step bench_extra 600 python "$ROOT/bench.py" $EXTRA_BENCH > "$OUT/${TAG}_bench_extra.json" 2> "$OUT/${TAG}_bench_extra.err"
+if [ "${RUN_TORCHRUN:-0}" = 1 ]; then
+  # rehearse the N>1 launch path on one GPU: 2 ranks, gloo all-gather, shared device
+  step torchrun2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 "$ROOT/bench.py" --gpus 2 --steps 2 --warmup 1 --dist-backend gloo > "$OUT/${TAG}_torchrun2.json" 2> "$OUT/${TAG}_torchrun2.err"
+fi
 for lib in ${VARIANTS:-}; do
   n=$(basename "$lib" .so)
   P1HIP_LIB="$ROOT/$lib" step "bench_$n" 600 python "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu > "$OUT/${TAG}_bench_$n.json" 2> "$OUT/${TAG}_bench_$n.err"
@@ -35,7 +39,7 @@ if [ "${SKIP_PMC:-0}" != 1 ]; then
   i=0
   for set in "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))
-    step pmc$i 600 rocprofv3 --pmc $set --kernel-include-regex k_scan_fast -d "$OUT/${TAG}_pmc$i" -o pmc --output-format csv -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu
+    step pmc$i 600 rocprofv3 --pmc $set --kernel-include-regex '^k_scan' -d "$OUT/${TAG}_pmc$i" -o pmc --output-format csv -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu
   done
 fi
 echo "== done"

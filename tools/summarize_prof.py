@@ -1,0 +1,64 @@
+"""Copy one GPU session's rocprofv3 outputs from gpurun_out/ into profiles/
+and write a JSON summary of the scan kernel's counters.
+
+usage: python tools/summarize_prof.py <TAG> [nonces_per_launch]
+  reads  gpurun_out/<TAG>_prof/run_kernel_stats.csv  (--kernel-trace --stats)
+         gpurun_out/<TAG>_pmc*/pmc_counter_collection.csv (--pmc passes)
+         gpurun_out/<TAG>_bench*.json, <TAG>_valu_*.jsonl
+  writes profiles/<TAG>_kernel_stats.csv, profiles/<TAG>_pmc_summary.json,
+         profiles/<TAG>_bench*.json, profiles/<TAG>_valu_*.jsonl
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag = sys.argv[1]
+    nonces = float(sys.argv[2]) if len(sys.argv) > 2 else 2.0**32
+    src = os.path.join(ROOT, "gpurun_out")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    ks = os.path.join(src, f"{tag}_prof", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        shutil.copy(ks, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    for f in glob.glob(os.path.join(src, f"{tag}_bench*.json")) + glob.glob(os.path.join(src, f"{tag}_valu_*.jsonl")):
+        shutil.copy(f, os.path.join(dst, os.path.basename(f)))
+    counters, durs = {}, []
+    for f in sorted(glob.glob(os.path.join(src, f"{tag}_pmc*", "*counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            if not r["Kernel_Name"].startswith("k_scan") and "k_scan_fast" not in r["Kernel_Name"]:
+                continue
+            counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    if not counters:
+        print("no PMC data for", tag)
+        return
+    avg = {k: sum(v) / len(v) for k, v in counters.items()}
+    dur = sum(durs) / len(durs)
+    out = {"tag": tag, "kernel": "k_scan", "avg_duration_s": dur, "counters_per_launch": avg}
+    if "GRBM_GUI_ACTIVE" in avg:
+        out["effective_clock_GHz"] = avg["GRBM_GUI_ACTIVE"] / 8 / dur / 1e9  # summed over 8 XCDs
+    if "SQ_INSTS_VALU" in avg:
+        out["valu_wave_instr_per_nonce"] = avg["SQ_INSTS_VALU"] * 64 / nonces
+        if "effective_clock_GHz" in out:
+            simd_cycles = dur * out["effective_clock_GHz"] * 1e9 * 1024
+            out["simd_cycles_per_valu_wave_instr"] = simd_cycles / avg["SQ_INSTS_VALU"]
+            out["valu_issue_frac_of_2cyc_peak"] = 2.0 / out["simd_cycles_per_valu_wave_instr"]
+    if "FETCH_SIZE" in avg or "WRITE_SIZE" in avg:
+        # FETCH_SIZE/WRITE_SIZE are KB; gfx950 FETCH_SIZE under-counts wide streaming reads 2x
+        # (MI355X_MICROARCH.md HBM section) -- this kernel has no such reads (kernel args,
+        # a <4 KB segment table via scalar loads, 16-B partial stores), so no correction applies.
+        out["hbm_bytes_per_launch"] = (avg.get("FETCH_SIZE", 0.0) + avg.get("WRITE_SIZE", 0.0)) * 1024
+    with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
