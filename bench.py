@@ -45,6 +45,20 @@ CONFIGS = {
 }
 
 
+def pmc_traffic():
+    """HBM bytes per k_scan launch from the newest committed rocprofv3 PMC
+    summary (profiles/*_pmc_summary.json, FETCH_SIZE + WRITE_SIZE of the c2
+    workload, collected in separate --pmc passes by tools/gpu_round.sh)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(msg, start, target_s):
     """Oracle restatement (format + full SHA-256 per nonce, the reference's
     per-nonce work) on the host cores, bounded sample."""
@@ -145,6 +159,7 @@ def main():
         hashes = total * args.steps
         value = hashes / elapsed / 1e9
         ms_per_step = elapsed * 1e3 / args.steps
+        traffic, traffic_src = pmc_traffic() if args.config == "c2" else (None, None)
         k_ms = stats["scan_kernel_ms"]
         k_n = stats["scan_launches"]
         achieved = stats["scan_alg_ops"] / (k_ms * 1e-3) if k_ms > 0 else 0.0
@@ -154,7 +169,9 @@ def main():
             "peak": VALU_PEAK_OPS / 1e12,
             "unit": "TOP/s",
             "frac": achieved / VALU_PEAK_OPS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes/launch (PMC FETCH_SIZE+WRITE_SIZE)",
+            "traffic_source": traffic_src,
             "kernel": "k_scan (one launch per scan covers every decade; algorithmic ops = 1384 x B_tail per nonce)",
             "alg_ops_per_nonce": ALG_OPS_PER_COMPRESSION * cfg["b_tail"],
             "avg_launch_ms": k_ms / k_n if k_n else None,

@@ -5,9 +5,9 @@
 //   Ch / Maj  -> one v_bitop3_b32 each (truth tables 0xCA / 0xE8)
 //   xor3      -> one v_bitop3_b32 (0x96) for the three rotations of S0/S1/s0/s1
 //   T1, a'    -> v_add3_u32 (selected by the compiler from the '+' chains)
-// gfx950 has no bitop3 builtin, so the three-input logic ops are one-line
-// non-volatile inline asm without a memory clobber (the compiler may still
-// hoist or CSE them).  Every helper folds to a constant when its inputs are
+// gfx950 has no bitop3 builtin and LLVM does not reliably form it inside the
+// round's sums, so the three are one-line inline asm (convergent for the
+// compiler: it never hoists them, so fast_thread hoists invariants by hand).  Every helper folds to a constant when its inputs are
 // compile-time constants (`__builtin_constant_p`, resolved after
 // unrolling/inlining), so zero words of the message schedule cost nothing.
 //
@@ -74,7 +74,9 @@ P1_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return a ^ b ^ c;
 }
 
-// Ch(e,f,g) = (e & f) ^ (~e & g)
+// Ch(e,f,g) = (e & f) ^ (~e & g).  (Plain C also becomes one bitop3 in
+// isolation, but inside the T1 sum LLVM rewrites the disjoint terms into
+// and + add and the loop grows by ~100 instructions per nonce -- measured.)
 P1_HD uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if (!P1_CONST3(e, f, g)) {
