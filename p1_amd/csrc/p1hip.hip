@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -224,6 +225,7 @@ struct Runtime {
   std::mutex mu;
   std::vector<Dev> devs;
   bool profiling = false;
+  bool use_rccl = true;
   p1hip_stats_t stats{};
 };
 
@@ -283,7 +285,12 @@ int init_locked(Runtime& R, const std::vector<int>& ords) {
     HIPCHK(hipMalloc(&d.d_gather, sizeof(Key) * nd));
     HIPCHK(hipHostMalloc(&d.h_res, sizeof(Key) * nd, hipHostMallocDefault));
   }
-  if (nd > 1) {
+  // P1HIP_NO_RCCL=1 (tests only): combine the per-device results through the
+  // host instead of RCCL, so the multi-device code path (threads, sharding,
+  // combine) can be exercised with the same GPU listed twice on a 1-GPU box.
+  const char* norccl = getenv("P1HIP_NO_RCCL");
+  R.use_rccl = !(norccl && norccl[0] == '1');
+  if (nd > 1 && R.use_rccl) {
     std::vector<ncclComm_t> comms(nd);
     NCCLCHK(ncclCommInitAll(comms.data(), nd, ords.data()));
     for (int i = 0; i < nd; ++i) R.devs[i].comm = comms[i];
@@ -498,11 +505,14 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
         if (!r && hipMemcpyAsync(d.d_res, &idk, sizeof idk, hipMemcpyHostToDevice, d.stream) != hipSuccess)
           r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(identity)");
       }
-      if (!r && nd > 1) {
+      if (!r && nd > 1 && R.use_rccl) {
         ncclResult_t nr = ncclAllGather(d.d_res, d.d_gather, 2, ncclUint64, d.comm, d.stream);
         if (nr != ncclSuccess) r = fail(P1HIP_ERR_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
       }
-      if (!r && i == 0) {
+      if (!r && nd > 1 && !R.use_rccl) {  // host combine (tests)
+        if (hipMemcpyAsync(R.devs[0].h_res + i, d.d_res, sizeof(Key), hipMemcpyDeviceToHost, d.stream) != hipSuccess)
+          r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(result)");
+      } else if (!r && i == 0) {
         const Key* src = nd > 1 ? d.d_gather : d.d_res;
         if (hipMemcpyAsync(d.h_res, src, sizeof(Key) * nd, hipMemcpyDeviceToHost, d.stream) != hipSuccess)
           r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(result)");

@@ -135,3 +135,21 @@ def test_init_variants(gpu):
     assert got == 1 and gpu.device_count() == 1
     gpu.init_devices([0])
     assert gpu.scan("msg", 0, 2) == (4754799531757243342, 1)
+
+
+def test_multi_device_path_on_one_gpu(gpu, oracle_mod, monkeypatch):
+    """p1hip_scan's multi-device code path (one host thread per device,
+    contiguous shards, combine) with GPU 0 listed three times; RCCL cannot
+    pair a GPU with itself, so the test combines through the host
+    (P1HIP_NO_RCCL=1, read at init)."""
+    monkeypatch.setenv("P1HIP_NO_RCCL", "1")
+    try:
+        gpu.init_devices([0, 0, 0])
+        assert gpu.device_count() == 3
+        for m, lo, hi in [(b"bradfitz", 0, 9999), (b"x" * 57, 10**9 - 4000, 10**9 + 4000),
+                          (b"msg", 0, 1), (b"msg", 5, 5), (b"msg", 9, 3)]:
+            assert gpu.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (m, lo, hi)
+        assert gpu.scan("bradfitz", 0, (1 << 32) - 1) == (5256245051, 1626825724)
+    finally:
+        monkeypatch.delenv("P1HIP_NO_RCCL")
+        gpu.init_devices([0])
