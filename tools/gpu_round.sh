@@ -23,6 +23,7 @@ step() {  # step <name> <timeout> <cmd...>
 [ "${SKIP_SMOKE:-0}" = 1 ] || step smoke 300 python -c "import sys; sys.path.insert(0, '$ROOT'); import __graft_entry__ as g; g.smoke()" > "$OUT/${TAG}_smoke.log" 2>&1
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 600 python "$ROOT/bench.py" ${BENCH_ARGS:-} > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
 [ -z "${EXTRA_BENCH:-}" ] || step bench_extra 600 python "$ROOT/bench.py" $EXTRA_BENCH > "$OUT/${TAG}_bench_extra.json" 2> "$OUT/${TAG}_bench_extra.err"
+[ "${RUN_SWEEP:-0}" != 1 ] || step sweep 900 python "$ROOT/tools/sweep.py" > "$OUT/${TAG}_sweep.jsonl" 2> "$OUT/${TAG}_sweep.err"
 if [ "${RUN_TORCHRUN:-0}" = 1 ]; then
   # rehearse the N>1 launch path on one GPU: 2 ranks, gloo all-gather, shared device
   step torchrun2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 "$ROOT/bench.py" --gpus 2 --steps 2 --warmup 1 --dist-backend gloo > "$OUT/${TAG}_torchrun2.json" 2> "$OUT/${TAG}_torchrun2.err"
