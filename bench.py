@@ -206,6 +206,17 @@ def main():
             "result": {"hash": result[0], "nonce": result[1], "consistent": consistent,
                        "matches_known": (tuple(result) == known) if known else None},
         }
+        # configs[0]'s request (client 'bradfitz' maxNonce 9999) as one
+        # drop-in call: per-request latency of p1hip_scan on a small job
+        lat = []
+        for _ in range(20):
+            t0 = time.perf_counter()
+            small = p1_amd.scan(b"bradfitz", 0, 9999)
+            lat.append(time.perf_counter() - t0)
+        lat.sort()
+        line["small_request"] = {"request": "bradfitz [0, 9999] (configs[0])", "result": list(small),
+                                 "matches_known": tuple(small) == (1419516646206828, 9898),
+                                 "median_latency_us": lat[len(lat) // 2] * 1e6}
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(msg, 1 << 31, args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -153,3 +153,35 @@ def test_multi_device_path_on_one_gpu(gpu, oracle_mod, monkeypatch):
     finally:
         monkeypatch.delenv("P1HIP_NO_RCCL")
         gpu.init_devices([0])
+
+
+def test_long_messages_and_limits(gpu, oracle_mod):
+    import ctypes
+
+    m = bytes((i * 131 + 7) % 251 for i in range(1 << 20))  # 1 MiB: 16384 midstate blocks on the host
+    for lo, hi in [(0, 3000), (10**11 - 1500, 10**11 + 1500)]:
+        assert gpu.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8)
+    lib = gpu.load()
+    h, n = ctypes.c_uint64(), ctypes.c_uint64()
+    assert lib.p1hip_scan(b"x", (1 << 28) + 1, 0, 1, ctypes.byref(h), ctypes.byref(n)) == -4
+
+
+def test_random_requests_vs_oracle(gpu, oracle_mod):
+    """Many small random requests (random bytes incl. non-UTF-8, random
+    lengths and ranges anywhere in u64), the way a server would send them."""
+    rnd = random.Random(2026)
+    for _ in range(300):
+        L = rnd.choice([rnd.randrange(0, 140), rnd.randrange(0, 2000)])
+        m = bytes(rnd.randrange(0, 256) for _ in range(L))
+        lo = rnd.choice([rnd.randrange(0, 10**6), rnd.randrange(0, U64_MAX), 10 ** rnd.randrange(1, 20) - rnd.randrange(0, 500)])
+        hi = min(lo + rnd.randrange(0, 3000), U64_MAX)
+        assert gpu.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (L, lo, hi)
+
+
+def test_reduce_pairs_large(gpu):
+    rnd = random.Random(9)
+    n = 1_000_003
+    hs = [rnd.randrange(0, U64_MAX) for _ in range(n)]
+    ns = [rnd.randrange(0, U64_MAX) for _ in range(n)]
+    want = min(zip(hs, ns))
+    assert gpu.reduce_pairs(hs, ns) == want
