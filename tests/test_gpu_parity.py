@@ -173,7 +173,8 @@ def test_random_requests_vs_oracle(gpu, oracle_mod):
     for _ in range(300):
         L = rnd.choice([rnd.randrange(0, 140), rnd.randrange(0, 2000)])
         m = bytes(rnd.randrange(0, 256) for _ in range(L))
-        lo = rnd.choice([rnd.randrange(0, 10**6), rnd.randrange(0, U64_MAX), 10 ** rnd.randrange(1, 20) - rnd.randrange(0, 500)])
+        lo = max(0, rnd.choice([rnd.randrange(0, 10**6), rnd.randrange(0, U64_MAX),
+                                10 ** rnd.randrange(1, 20) - rnd.randrange(0, 500)]))
         hi = min(lo + rnd.randrange(0, 3000), U64_MAX)
         assert gpu.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (L, lo, hi)
 
