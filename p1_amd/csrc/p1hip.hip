@@ -257,6 +257,8 @@ void shutdown_locked(Runtime& R) {
   R.devs.clear();
 }
 
+int init_devs(Runtime& R, const std::vector<int>& ords);
+
 int init_locked(Runtime& R, const std::vector<int>& ords) {
   if (!R.devs.empty()) {
     bool same = R.devs.size() == ords.size();
@@ -264,6 +266,16 @@ int init_locked(Runtime& R, const std::vector<int>& ords) {
     if (same) return P1HIP_OK;
     shutdown_locked(R);
   }
+  const int rc = init_devs(R, ords);
+  if (rc != P1HIP_OK) {  // never leave a half-initialised device list behind
+    const std::string keep = g_err;
+    shutdown_locked(R);
+    g_err = keep;
+  }
+  return rc;
+}
+
+int init_devs(Runtime& R, const std::vector<int>& ords) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
     return fail(P1HIP_ERR_NO_DEVICE, "no HIP device visible");
@@ -500,10 +512,10 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
       if (active[i]) {
         r = run_range(d, msg, msg_len, slo[i], shi[i], R.profiling);
       } else {
+        // empty shard: contribute the identity key (all ones)
         if (hipSetDevice(d.ordinal) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipSetDevice");
-        const Key idk = {~0ull, ~0ull};
-        if (!r && hipMemcpyAsync(d.d_res, &idk, sizeof idk, hipMemcpyHostToDevice, d.stream) != hipSuccess)
-          r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(identity)");
+        if (!r && hipMemsetAsync(d.d_res, 0xFF, sizeof(Key), d.stream) != hipSuccess)
+          r = fail(P1HIP_ERR_HIP, "hipMemsetAsync(identity)");
       }
       if (!r && nd > 1 && R.use_rccl) {
         ncclResult_t nr = ncclAllGather(d.d_res, d.d_gather, 2, ncclUint64, d.comm, d.stream);

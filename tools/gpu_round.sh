@@ -24,6 +24,7 @@ step() {  # step <name> <timeout> <cmd...>
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 600 python "$ROOT/bench.py" ${BENCH_ARGS:-} > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
 [ -z "${EXTRA_BENCH:-}" ] || step bench_extra 600 python "$ROOT/bench.py" $EXTRA_BENCH > "$OUT/${TAG}_bench_extra.json" 2> "$OUT/${TAG}_bench_extra.err"
 [ "${RUN_SWEEP:-0}" != 1 ] || step sweep 900 python "$ROOT/tools/sweep.py" > "$OUT/${TAG}_sweep.jsonl" 2> "$OUT/${TAG}_sweep.err"
+[ "${RUN_SERVER:-0}" != 1 ] || step bench_server 900 python "$ROOT/tools/bench_server.py" > "$OUT/${TAG}_bench_server.json" 2> "$OUT/${TAG}_bench_server.err"
 if [ "${RUN_TORCHRUN:-0}" = 1 ]; then
   # rehearse the N>1 launch path on one GPU: 2 ranks, gloo all-gather, shared device
   step torchrun2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 "$ROOT/bench.py" --gpus 2 --steps 2 --warmup 1 --dist-backend gloo > "$OUT/${TAG}_torchrun2.json" 2> "$OUT/${TAG}_torchrun2.err"
