@@ -50,6 +50,13 @@ __global__ __launch_bounds__(256) void k_valu(uint32_t* out, uint32_t seed) {
       else if (OP == 22) P1_BODY4("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca");
       else if (OP == 23) P1_BODY4("v_bitop3_b16 %0, %0, %1, %2 bitop3:0x96");
       else if (OP == 24) P1_BODY4("v_mov_b32_e32 %0, %1");
+      else if (OP == 26) {  // 64-bit shift of a register pair (r, r): low word = rotr
+        uint64_t v = ((uint64_t)r[c] << 32) | r[c];
+        asm volatile("v_lshrrev_b64 %0, 7, %0\n\tv_lshrrev_b64 %0, 9, %0\n\tv_lshrrev_b64 %0, 3, %0\n\tv_lshrrev_b64 %0, 5, %0"
+                     : "+v"(v));
+        r[c] = (uint32_t)v ^ (uint32_t)(v >> 32);
+      }
+      else if (OP == 27) P1_BODY4("v_add_u32_e32 %0, 0x428a2f98, %0");
       else if (OP == 25) {  // half alignbit, half bitop3 interleaved
         asm volatile("v_alignbit_b32 %0, %0, %0, 7\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\t"
                      "v_alignbit_b32 %0, %0, %0, 9\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0xca"
@@ -103,6 +110,7 @@ int main() {
   RUN(9, "v_xad_u32"); RUN(10, "v_or3_b32"); RUN(11, "v_lshl_add_u32"); RUN(12, "v_add_lshl_u32");
   RUN(13, "v_and_or_b32"); RUN(14, "v_bfi_b32"); RUN(18, "v_pk_add_u16"); RUN(19, "v_bfe_u32");
   RUN(20, "v_mad_u32_u24"); RUN(21, "v_cndmask_b32_e64"); RUN(24, "v_mov_b32"); RUN(25, "alignbit/bitop3 mix");
+  RUN(26, "v_lshrrev_b64 (+2 VALU per 4)"); RUN(27, "v_add_u32_e32 literal");
 #undef RUN
   return 0;
 }
