@@ -106,7 +106,10 @@ def main():
     import torch.distributed as dist
 
     import p1_amd
+    from p1_amd.build import ensure_built
     from p1_amd.dist import distributed_scan
+
+    ensure_built()
 
     ngpu = torch.cuda.device_count()
     gpu = local % ngpu if args.dist_backend == "gloo" else local  # gloo rehearsal may share a GPU

@@ -11,6 +11,10 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box)")
+    # a fresh checkout builds once (normally everything is prebuilt by `make`)
+    from p1_amd.build import ensure_built
+
+    ensure_built()
 
 
 @pytest.fixture(scope="session")
