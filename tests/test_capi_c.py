@@ -19,7 +19,8 @@ def _build(tmp_path):
 
 def test_header_is_c99_and_links(tmp_path):
     exe = _build(tmp_path)
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", "0").split(",")[0])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     try:
         import torch
 
@@ -35,6 +36,7 @@ def test_header_is_c99_and_links(tmp_path):
 @pytest.mark.gpu
 def test_c_client_on_gpu(tmp_path):
     exe = _build(tmp_path)
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", "0").split(",")[0])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip() == "Result 1419516646206828 9898"

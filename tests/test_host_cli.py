@@ -19,7 +19,9 @@ def built():
 
 
 def run(args, stdin=None):
-    return subprocess.run([MINER] + args, input=stdin, capture_output=True, text=True, timeout=600)
+    # one visible GPU: without --device the miner opens every visible device
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", "0").split(",")[0])
+    return subprocess.run([MINER] + args, input=stdin, capture_output=True, text=True, timeout=600, env=env)
 
 
 def test_json_wire_format_matches_go():
