@@ -11,7 +11,9 @@ the (hash, nonce) result on the host.  With N GPUs (torchrun, one process per
 GPU) the job range is [0, N*2^32), sharded contiguously (weak scaling); the
 16-byte per-rank results are all-gathered over RCCL (torch.distributed
 "nccl") and reduced with the lexicographic (hash, nonce) min.  `--config c3`
-selects configs[2] (120-byte msg, 2^34 nonces per GPU, 2 tail blocks).
+selects configs[2] (120-byte msg, 2^34 nonces per GPU, 2 tail blocks);
+`--config c4` selects configs[3] (the fixed [0, 2^38) job split over the GPUs,
+strong scaling).
 
 Prints ONE JSON line on rank 0.
 """
@@ -41,6 +43,10 @@ CONFIGS = {
            "known": {1: (5256245051, 1626825724)}},
     "c3": {"msg": b"cmu440-p1-" * 12, "per_gpu": 1 << 34, "b_tail": 2,
            "desc": "configs[2]: 120-byte msg, host midstate, nonces [0,2^34) per GPU, 2 tail blocks/nonce",
+           "known": {}},
+    # configs[3]: the fixed 2^38 job split over however many GPUs run (strong scaling)
+    "c4": {"msg": b"bradfitz", "total": 1 << 38, "b_tail": 1,
+           "desc": "configs[3]: 8-byte msg 'bradfitz', nonces [0,2^38) split contiguously over the GPUs",
            "known": {}},
 }
 
@@ -122,7 +128,7 @@ def main():
     p1_amd.init_devices([gpu])
 
     msg = cfg["msg"]
-    total = cfg["per_gpu"] * world
+    total = cfg["total"] if "total" in cfg else cfg["per_gpu"] * world
     shard = p1_amd.shard_range(0, total - 1, rank, world)
     dev = torch.device("cuda", gpu)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
@@ -192,14 +198,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if "total" in cfg else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
             "config": {
                 "workload": cfg["desc"],
                 "msg_len": len(msg),
-                "nonces_per_gpu": cfg["per_gpu"],
+                "nonces_per_gpu": total // world,
                 "job_range": [0, total - 1],
                 "parallelism": f"range-shard x{world}" + (
                     (" + RCCL all-gather" if args.dist_backend == "nccl" else " + gloo all-gather (rehearsal)")

@@ -186,3 +186,16 @@ def test_reduce_pairs_large(gpu):
     ns = [rnd.randrange(0, U64_MAX) for _ in range(n)]
     want = min(zip(hs, ns))
     assert gpu.reduce_pairs(hs, ns) == want
+
+
+def test_config4_range_on_one_gpu_multi_batch(gpu, oracle_mod):
+    """configs[3]'s whole [0, 2^38) on one GPU: > 2^20 workgroups, so the scan
+    is split into several launches (batches).  Checked by size-independent
+    properties: re-hash of the result and min of two halves (single batch
+    each)."""
+    hi = (1 << 38) - 1
+    h, n = gpu.scan("bradfitz", 0, hi)
+    assert oracle_mod.hash("bradfitz", n) == h
+    a = gpu.scan("bradfitz", 0, (1 << 37) - 1)
+    b = gpu.scan("bradfitz", 1 << 37, hi)
+    assert min(a, b) == (h, n)
