@@ -51,6 +51,38 @@ CONFIGS = {
 }
 
 
+# The algorithmic SHA-256 compression (SURVEY.md 8(d)'s 1384 ops) by
+# instruction class: 64 rounds x (6 rotr, 4 bitop3, 3 add3, 1 add) +
+# 48 schedule words x (4 rotr, 2 shr, 2 bitop3, 1 add3, 1 add) + 8 adds.
+ALG_MIX = {"v_alignbit_b32": 576, "v_bitop3_b32": 352, "v_add3_u32": 240, "v_add_u32": 120,
+           "v_lshrrev_b32": 96}
+VALU_PEAK_PROFILE = "profiles/r01_valu_peak.jsonl"
+
+
+def mix_roofline():
+    """Hashes/s one MI355X would reach if every instruction of the
+    algorithmic compression issued at its own measured peak rate
+    (tools/valu_peak, 8 waves/SIMD, lane-ops/clk/CU) at 2.4 GHz."""
+    path = os.path.join(ROOT, VALU_PEAK_PROFILE)
+    if not os.path.exists(path):
+        return None
+    rate = {}
+    names = {"v_alignbit_b32 (x,x,imm)": "v_alignbit_b32", "v_bitop3_b32 0x96": "v_bitop3_b32",
+             "v_add3_u32": "v_add3_u32", "v_add_u32_e32": "v_add_u32", "v_lshrrev_b32_e32": "v_lshrrev_b32"}
+    with open(path) as f:
+        for line in f:
+            if not line.startswith("{"):
+                continue
+            d = json.loads(line)
+            if d.get("instr") in names and d.get("blocks_per_cu_wave_slots") == 8:
+                rate[names[d["instr"]]] = d["per_cu_per_clk_at_2.4GHz"]
+    if set(rate) != set(ALG_MIX):
+        return None
+    cu_cycles = sum(n / rate[k] for k, n in ALG_MIX.items())  # per nonce per compression
+    return {"peak_GH_s_per_block": 256 * 2.4e9 / cu_cycles / 1e9, "cu_cycles_per_compression": cu_cycles,
+            "rates_lane_ops_per_clk_cu": rate, "source": VALU_PEAK_PROFILE}
+
+
 def pmc_traffic():
     """HBM bytes per k_scan launch from the newest committed rocprofv3 PMC
     summary (profiles/*_pmc_summary.json, FETCH_SIZE + WRITE_SIZE of the c2
@@ -189,6 +221,12 @@ def main():
             "frac_vs_survey_peak": achieved / SURVEY_PEAK_OPS,
             "fast_nonce_share": stats["fast_nonces"] / max(1, stats["fast_nonces"] + stats["generic_nonces"]),
         }
+        mix = mix_roofline()
+        if mix and k_ms > 0:
+            khs = stats["scan_nonces"] / (k_ms * 1e-3) / 1e9
+            mix["peak_GH_s"] = mix["peak_GH_s_per_block"] / cfg["b_tail"]
+            mix["frac"] = khs / mix["peak_GH_s"]
+            roofline["mix_roofline"] = mix
         line = {
             "metric": "SHA-256 nonce-hashes/sec (GH/s)",
             "value": value,
