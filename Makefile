@@ -2,13 +2,42 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall
+LLVM ?= /opt/rocm/lib/llvm/bin
 CSRC := p1_amd/csrc
-HDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/planner.hpp $(CSRC)/fast_variants.inc include/p1hip.h
+HDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/planner.hpp $(CSRC)/fast_variants.inc \
+        $(CSRC)/scan_abi.hpp include/p1hip.h
+# device code: HIP C++ -> gfx950 assembly -> tools/isa_post.py peephole
+# (VOP2 -> VOP3 encodings of full-rate integer ops, every inner loop started
+# at 4 mod 8 bytes; see DESIGN.md "Build") -> assembled + linked code object,
+# embedded in libp1hip.so
+DEVFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) --cuda-device-only -Wall $(DEVEXTRA)
+ISAPOST ?= --align-loops=3 --loop-offset=4
+BUILD := build
 
 all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server
 
-p1_amd/libp1hip.so: $(CSRC)/p1hip.hip $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/p1hip.hip -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+$(BUILD)/p1hip_kernels.s: $(CSRC)/p1hip_kernels.hip $(HDRS)
+	mkdir -p $(BUILD)
+	$(HIPCC) $(DEVFLAGS) -S -o $@ $(CSRC)/p1hip_kernels.hip
+
+$(BUILD)/p1hip_kernels.post.s: $(BUILD)/p1hip_kernels.s tools/isa_post.py
+	python3 tools/isa_post.py $< $@ $(ISAPOST)
+
+$(BUILD)/p1hip_kernels.o: $(BUILD)/p1hip_kernels.post.s
+	$(LLVM)/clang -cc1as -triple amdgcn-amd-amdhsa -filetype obj -target-cpu $(ARCH) -mrelocation-model pic -o $@ $<
+
+$(BUILD)/p1hip_kernels.hsaco: $(BUILD)/p1hip_kernels.o
+	$(LLVM)/ld.lld -m elf64_amdgpu --no-undefined -shared -o $@ $<
+
+$(BUILD)/p1hip_kernels_blob.o: $(CSRC)/p1hip_kernels_blob.S $(BUILD)/p1hip_kernels.hsaco
+	gcc -c -fPIC -DP1HIP_KERNELS_CO='"$(CURDIR)/$(BUILD)/p1hip_kernels.hsaco"' -o $@ $<
+
+$(BUILD)/p1hip_host.o: $(CSRC)/p1hip.hip $(HDRS)
+	mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $(CSRC)/p1hip.hip
+
+p1_amd/libp1hip.so: $(BUILD)/p1hip_host.o $(BUILD)/p1hip_kernels_blob.o
+	$(HIPCC) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 # C++ host mirror of the reference's bitcoin package + miner loop (stdio)
 p1_amd/p1miner: p1_amd/host/p1miner.cpp p1_amd/host/bitcoin.cpp p1_amd/host/bitcoin.hpp include/p1hip.h p1_amd/libp1hip.so
@@ -24,17 +53,20 @@ tools/p1emu: tools/p1emu.cpp $(HDRS)
 oracle:
 	$(MAKE) -C oracle
 
-# A/B tuning builds (not used unless P1HIP_LIB points at one)
-variants: p1_amd/variants/libp1hip_w4.so p1_amd/variants/libp1hip_w6.so p1_amd/variants/libp1hip_w8.so
-p1_amd/variants/libp1hip_w%.so: $(CSRC)/p1hip.hip $(HDRS)
+# A/B tuning builds (not used unless P1HIP_LIB points at one):
+#   make variant NAME=x DEVEXTRA='-DP1_FAST_WAVES=5' ISAPOST='--no-e64'
+variant:
+	$(MAKE) BUILD=build/var_$(NAME) DEVEXTRA="$(DEVEXTRA)" ISAPOST="$(ISAPOST)" build/var_$(NAME)/p1hip_kernels_blob.o build/var_$(NAME)/p1hip_host.o
 	mkdir -p p1_amd/variants
-	$(HIPCC) $(HIPFLAGS) -DP1_FAST_WAVES=$* -shared -o $@ $(CSRC)/p1hip.hip -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) -shared -fPIC -o p1_amd/variants/libp1hip_$(NAME).so build/var_$(NAME)/p1hip_host.o build/var_$(NAME)/p1hip_kernels_blob.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
-# ISA + resource report of the scan kernels (for DESIGN.md / profiling)
-isa: $(CSRC)/p1hip.hip $(HDRS)
-	mkdir -p build/isa && cd build/isa && $(HIPCC) $(HIPFLAGS) -c ../../$(CSRC)/p1hip.hip -o p1hip.o -save-temps -Rpass-analysis=kernel-resource-usage 2> resource.txt
+# ISA + resource report of the scan kernels (for DESIGN.md / profiling):
+# build/p1hip_kernels.post.s is the exact assembly that ships
+isa: $(BUILD)/p1hip_kernels.post.s
+	$(HIPCC) $(DEVFLAGS) -c -o /dev/null $(CSRC)/p1hip_kernels.hip -Rpass-analysis=kernel-resource-usage 2> $(BUILD)/resource.txt || true
 
 clean:
 	rm -f p1_amd/libp1hip.so tools/p1emu p1_amd/p1miner p1_amd/p1server
+	rm -rf $(BUILD)/p1hip_kernels* $(BUILD)/p1hip_host.o
 	$(MAKE) -C oracle clean
-.PHONY: all oracle clean isa variants
+.PHONY: all oracle clean isa variant

@@ -1,5 +1,5 @@
-// p1hip.hip -- libp1hip.so: gfx950 kernels, launch orchestration and the C ABI
-// declared in include/p1hip.h.
+// p1hip.hip -- libp1hip.so: host runtime (planning, launch orchestration,
+// multi-device combine) and the C ABI declared in include/p1hip.h.
 //
 // Replaces the miner's scan loop /root/reference/src/github.com/cmu440/bitcoin/
 // miner/miner.go:56-63 (see include/p1hip.h for the exact contract).
@@ -7,13 +7,11 @@
 // Device pipeline of one p1hip_scan on one device (one HIP stream):
 //   planner.hpp  -> list of pieces (fast: one thread per 10^k nonces;
 //                   generic: one thread per nonce, for ragged edges)
-//   k_scan       -> one launch, one segment per piece (variant chosen per
-//                   workgroup from the segment table: fast_thread<FV,NV,TRAIL>
-//                   or generic_thread)
-//                -> per-thread best (hash, nonce) -> wave argmin with DPP
-//                   (quad_perm, row_ror) + ds_swizzle + readlane -> LDS across
-//                   the 4 waves -> one 16-byte partial per workgroup
+//   k_scan       -> one launch, one segment per piece (p1hip_kernels.hip)
 //   k_reduce     -> one workgroup folds all partials into the device result
+// The kernels live in a gfx950 code object built from p1hip_kernels.hip via
+// assembly + tools/isa_post.py (Makefile) and embedded in this library
+// (p1hip_kernels_blob.S); each device loads it with hipModuleLoadData.
 // Several devices: contiguous shards, one host thread per device, RCCL
 // all-gather of the 16-byte results (ncclCommInitAll), host lexicographic min.
 #include <hip/hip_runtime.h>
@@ -31,138 +29,12 @@
 
 #include "../../include/p1hip.h"
 #include "planner.hpp"
+#include "scan_abi.hpp"
+
+// the embedded gfx950 code object (p1hip_kernels_blob.S)
+extern "C" const unsigned char p1hip_kernels_co[];
 
 using namespace p1;
-
-// ----------------------------------------------------------------------------
-// Wave / workgroup argmin over Key = (hash, nonce), lexicographic.
-// ----------------------------------------------------------------------------
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
-}
-
-template <int CTRL>
-__device__ __forceinline__ Key key_dpp(const Key& k) {
-  Key o;
-  o.h = ((uint64_t)dpp<CTRL>((uint32_t)(k.h >> 32)) << 32) | dpp<CTRL>((uint32_t)k.h);
-  o.n = ((uint64_t)dpp<CTRL>((uint32_t)(k.n >> 32)) << 32) | dpp<CTRL>((uint32_t)k.n);
-  return o;
-}
-
-__device__ __forceinline__ uint32_t swz_xor16(uint32_t v) {
-  // ds_swizzle bit-mask mode: and 0x1f, or 0, xor 0x10 (within 32 lanes)
-  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
-}
-
-__device__ __forceinline__ Key key_min(const Key& a, const Key& b) { return key_lt(b, a) ? b : a; }
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// All 64 lanes must be active.  Returns the wave minimum (wave-uniform).
-__device__ __forceinline__ Key wave_min(Key k) {
-  k = key_min(k, key_dpp<0xB1>(k));   // quad_perm [1,0,3,2]  (xor 1)
-  k = key_min(k, key_dpp<0x4E>(k));   // quad_perm [2,3,0,1]  (xor 2)
-  k = key_min(k, key_dpp<0x124>(k));  // row_ror:4
-  k = key_min(k, key_dpp<0x128>(k));  // row_ror:8  -> every lane holds its row min
-  Key o;
-  o.h = ((uint64_t)swz_xor16((uint32_t)(k.h >> 32)) << 32) | swz_xor16((uint32_t)k.h);
-  o.n = ((uint64_t)swz_xor16((uint32_t)(k.n >> 32)) << 32) | swz_xor16((uint32_t)k.n);
-  k = key_min(k, o);                  // halves of 32 lanes
-  Key a, b;
-  a.h = readlane64(k.h, 0);  a.n = readlane64(k.n, 0);
-  b.h = readlane64(k.h, 32); b.n = readlane64(k.n, 32);
-  return key_min(a, b);
-}
-
-template <int NT>
-__device__ __forceinline__ void block_min_store(Key k, Key* out) {
-  __shared__ Key sk[NT / 64];
-  k = wave_min(k);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0) sk[wid] = k;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    Key b = sk[0];
-#pragma unroll
-    for (int w = 1; w < NT / 64; ++w) b = key_min(b, sk[w]);
-    *out = b;
-  }
-}
-
-// ----------------------------------------------------------------------------
-// Kernels
-// ----------------------------------------------------------------------------
-// Minimum waves per SIMD the register allocator must leave room for
-// (tuned on MI355X); override with -DP1_FAST_WAVES=n.
-#ifndef P1_FAST_WAVES
-#define P1_FAST_WAVES 4
-#endif
-
-// Variant id of a fast segment; kGenericKind marks a generic segment.
-__host__ __device__ constexpr uint32_t variant_id(int fv, int nv, bool trail) {
-  return (trail ? 64u : 0u) + (uint32_t)fv * 2u + (uint32_t)(nv - 1);
-}
-constexpr uint32_t kGenericKind = 255;
-
-// One segment of a scan launch: a contiguous run of workgroups that all do
-// the same kind of work (one decade piece).
-struct Segment {
-  uint32_t kind;    // variant_id(...) or kGenericKind
-  uint32_t block0;  // first workgroup of the segment within the launch
-  uint32_t pad[2];
-  FastArgs fa;
-  GenArgs ga;
-};
-
-// The scan kernel: every workgroup finds its segment (wave-uniform scalar
-// loop over the table), runs that segment's per-thread work and writes one
-// 16-byte partial.  All decades of a scan -- and their ragged edges -- share
-// one launch, so there is one grid drain per scan, filled by the short
-// segments that are placed last.
-__global__ __launch_bounds__(kBlock, P1_FAST_WAVES) void k_scan(const Segment* __restrict__ segs, uint32_t nseg,
-                                                                Key* __restrict__ part) {
-  const uint32_t b = blockIdx.x;
-  uint32_t si = 0;
-  while (si + 1 < nseg && segs[si + 1].block0 <= b) ++si;
-  const Segment& S = segs[si];
-  const uint32_t local = (b - S.block0) * kBlock + threadIdx.x;
-  Key k;
-  switch (S.kind) {
-#define P1_CASE(FV, NV, TR)                         \
-  case variant_id(FV, NV, TR):                      \
-    k = fast_thread<FV, NV, TR>(S.fa, local);       \
-    break;
-#include "fast_variants.inc"
-#undef P1_CASE
-    default:
-      k = generic_thread(S.ga, local);
-      break;
-  }
-  block_min_store<kBlock>(k, part + b);
-}
-
-constexpr int kReduceThreads = 1024;
-
-__global__ __launch_bounds__(kReduceThreads) void k_reduce(const Key* __restrict__ part, uint32_t n,
-                                                           Key* __restrict__ out) {
-  Key b = {~0ull, ~0ull};
-  for (uint32_t i = threadIdx.x; i < n; i += kReduceThreads) b = key_min(b, part[i]);
-  block_min_store<kReduceThreads>(b, out);
-}
-
-// test hook: one crafted pair per thread -> per-workgroup partials
-__global__ __launch_bounds__(kBlock) void k_pairs(const uint64_t* __restrict__ hs, const uint64_t* __restrict__ ns,
-                                                  uint64_t n, Key* __restrict__ part) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  Key k = {~0ull, ~0ull};
-  if (i < n) { k.h = hs[i]; k.n = ns[i]; }
-  block_min_store<kBlock>(k, part + blockIdx.x);
-}
 
 static bool has_variant(int fv, int nv, bool trail) {
 #define P1_CASE(FV, NV, TR) \
@@ -213,6 +85,8 @@ struct Dev {
   Segment* h_seg = nullptr;     // pinned staging for the tables
   size_t seg_cap = 0;           // launch slots allocated
   ncclComm_t comm = nullptr;
+  hipModule_t mod = nullptr;    // embedded code object, loaded on this device
+  hipFunction_t f_scan = nullptr, f_reduce = nullptr, f_pairs = nullptr;
   std::vector<hipEvent_t> evs;  // profiling event pool (pairs)
   // per-scan accounting filled by run_range
   uint64_t fast_launches = 0, fast_nonces = 0, fast_ops = 0, gen_launches = 0, gen_nonces = 0;
@@ -248,6 +122,7 @@ int dev_release(Dev& d) {
   if (d.d_gather) (void)hipFree(d.d_gather);
   if (d.h_res) (void)hipHostFree(d.h_res);
   if (d.stream) (void)hipStreamDestroy(d.stream);
+  if (d.mod) (void)hipModuleUnload(d.mod);
   d = Dev();
   return 0;
 }
@@ -293,6 +168,10 @@ int init_devs(Runtime& R, const std::vector<int>& ords) {
     d.ordinal = ords[i];
     HIPCHK(hipSetDevice(d.ordinal));
     HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HIPCHK(hipModuleLoadData(&d.mod, p1hip_kernels_co));
+    HIPCHK(hipModuleGetFunction(&d.f_scan, d.mod, "k_scan"));
+    HIPCHK(hipModuleGetFunction(&d.f_reduce, d.mod, "k_reduce"));
+    HIPCHK(hipModuleGetFunction(&d.f_pairs, d.mod, "k_pairs"));
     HIPCHK(hipMalloc(&d.d_res, sizeof(Key)));
     HIPCHK(hipMalloc(&d.d_gather, sizeof(Key) * nd));
     HIPCHK(hipHostMalloc(&d.h_res, sizeof(Key) * nd, hipHostMallocDefault));
@@ -308,6 +187,13 @@ int init_devs(Runtime& R, const std::vector<int>& ords) {
     for (int i = 0; i < nd; ++i) R.devs[i].comm = comms[i];
   }
   return P1HIP_OK;
+}
+
+// hipModuleLaunchKernel with the arguments as a pointer array
+template <typename... Args>
+hipError_t launch(hipFunction_t f, uint32_t blocks, uint32_t threads, hipStream_t st, Args... args) {
+  void* params[] = {(void*)&args...};
+  return hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, 0, st, params, nullptr);
 }
 
 int ensure_init(Runtime& R) {
@@ -409,9 +295,8 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
       }
       HIPCHK(hipEventRecord(d.evs[nev], d.stream));
     }
-    hipLaunchKernelGGL(k_scan, dim3(B.blocks), dim3(kBlock), 0, d.stream, ds, (uint32_t)B.count,
-                       d.d_part + part_off);
-    HIPCHK(hipGetLastError());
+    HIPCHK(launch(d.f_scan, B.blocks, kBlock, d.stream, (const Segment*)ds, (uint32_t)B.count,
+                  (Key*)(d.d_part + part_off)));
     if (profiling) {
       HIPCHK(hipEventRecord(d.evs[nev + 1], d.stream));
       nev += 2;
@@ -421,8 +306,7 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
     d.scan_nonces += nonces;
     d.scan_ops += ops;
   }
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, d.stream, d.d_part, total_blocks, d.d_res);
-  HIPCHK(hipGetLastError());
+  HIPCHK(launch(d.f_reduce, 1, kReduceThreads, d.stream, (const Key*)d.d_part, total_blocks, d.d_res));
   if (profiling && nev) {
     HIPCHK(hipEventSynchronize(d.evs[nev - 1]));
     for (size_t i = 0; i < nev; i += 2) {
@@ -590,10 +474,8 @@ int p1hip_reduce_pairs(const uint64_t* hashes, const uint64_t* nonces, size_t n,
     HIPCHK(hipMalloc(&dp, (size_t)blocks * sizeof(Key)));
     HIPCHK(hipMemcpyAsync(dh, hashes, n * 8, hipMemcpyHostToDevice, d.stream));
     HIPCHK(hipMemcpyAsync(dn, nonces, n * 8, hipMemcpyHostToDevice, d.stream));
-    hipLaunchKernelGGL(k_pairs, dim3(blocks), dim3(kBlock), 0, d.stream, dh, dn, (uint64_t)n, dp);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, d.stream, dp, blocks, d.d_res);
-    HIPCHK(hipGetLastError());
+    HIPCHK(launch(d.f_pairs, blocks, kBlock, d.stream, (const uint64_t*)dh, (const uint64_t*)dn, (uint64_t)n, dp));
+    HIPCHK(launch(d.f_reduce, 1, kReduceThreads, d.stream, (const Key*)dp, blocks, d.d_res));
     HIPCHK(hipMemcpyAsync(d.h_res, d.d_res, sizeof(Key), hipMemcpyDeviceToHost, d.stream));
     HIPCHK(hipStreamSynchronize(d.stream));
     res = d.h_res[0];
@@ -630,7 +512,7 @@ void p1hip_reset_stats(void) {
 
 const char* p1hip_last_error(void) { return g_err.c_str(); }
 
-const char* p1hip_version(void) { return "p1hip 0.1 gfx950"; }
+const char* p1hip_version(void) { return "p1hip 0.2 gfx950"; }
 
 void p1hip_shutdown(void) {
   Runtime& R = rt();

@@ -1,0 +1,32 @@
+// scan_abi.hpp -- what the host runtime (p1hip.hip) and the device code
+// object (p1hip_kernels.hip) agree on: the segment table of one k_scan launch,
+// variant ids and launch shapes.  The kernels are loaded by name from the
+// embedded code object (hipModuleLoadData), so this header IS their ABI.
+#pragma once
+#include "scan_core.hpp"
+
+namespace p1 {
+
+// Variant id of a fast segment; kGenericKind marks a generic segment.
+P1_HD constexpr uint32_t variant_id(int fv, int nv, bool trail) {
+  return (trail ? 64u : 0u) + (uint32_t)fv * 2u + (uint32_t)(nv - 1);
+}
+constexpr uint32_t kGenericKind = 255;
+
+// One segment of a scan launch: a contiguous run of workgroups that all do
+// the same kind of work (one decade piece).
+struct Segment {
+  uint32_t kind;    // variant_id(...) or kGenericKind
+  uint32_t block0;  // first workgroup of the segment within the launch
+  uint32_t pad[2];
+  FastArgs fa;
+  GenArgs ga;
+};
+
+constexpr int kReduceThreads = 1024;  // k_reduce: one workgroup
+
+// Kernel entry points (extern "C" names in the code object):
+//   k_scan(const Segment* segs, uint32_t nseg, Key* part)            grid: sum of segment blocks x kBlock
+//   k_reduce(const Key* part, uint32_t n, Key* out)                  grid: 1 x kReduceThreads
+//   k_pairs(const uint64_t* hs, const uint64_t* ns, uint64_t n, Key* part)  grid: ceil(n/kBlock) x kBlock
+}  // namespace p1

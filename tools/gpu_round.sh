@@ -35,13 +35,13 @@ for lib in ${VARIANTS:-}; do
 done
 cd /tmp && export TMPDIR=/tmp
 if [ "${SKIP_PROF:-0}" != 1 ]; then
-  step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu
+  step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-small-request
 fi
 if [ "${SKIP_PMC:-0}" != 1 ]; then
   i=0
   for set in "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))
-    step pmc$i 600 rocprofv3 --pmc $set --kernel-include-regex '^k_scan' -d "$OUT/${TAG}_pmc$i" -o pmc --output-format csv -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu
+    step pmc$i 600 rocprofv3 --pmc $set --kernel-include-regex '^k_scan' -d "$OUT/${TAG}_pmc$i" -o pmc --output-format csv -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu --no-small-request
   done
 fi
 echo "== done"

@@ -31,8 +31,14 @@ def main():
         shutil.copy(f, os.path.join(dst, os.path.basename(f)))
     counters, durs = {}, []
     for f in sorted(glob.glob(os.path.join(src, f"{tag}_pmc*", "*counter_collection.csv"))):
-        for r in csv.DictReader(open(f)):
-            if not r["Kernel_Name"].startswith("k_scan") and "k_scan_fast" not in r["Kernel_Name"]:
+        rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("k_scan")]
+        if not rows:
+            continue
+        # only the workload's own launches (largest grid); bench.py also times
+        # small configs[0]-sized requests whose launches are not the roofline kernel
+        gmax = max(int(r["Grid_Size"]) for r in rows)
+        for r in rows:
+            if int(r["Grid_Size"]) != gmax:
                 continue
             counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
