@@ -11,7 +11,7 @@ HDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/planner.hpp $(CSRC)
 # at 4 mod 8 bytes; see DESIGN.md "Build") -> assembled + linked code object,
 # embedded in libp1hip.so
 DEVFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) --cuda-device-only -Wall $(DEVEXTRA)
-ISAPOST ?= --align-loops=3 --loop-offset=4
+ISAPOST ?= --align-loops=3 --loop-offset=4 --loop-parity
 BUILD := build
 
 all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server

@@ -1,36 +1,63 @@
 #!/usr/bin/env python3
-"""Peephole pass over the gfx950 assembly of the scan kernels.
+"""Peephole pass over the gfx950 assembly of the scan kernels (build step,
+Makefile: build/p1hip_kernels.s -> build/p1hip_kernels.post.s).
 
 usage: isa_post.py IN.s OUT.s [--no-e64] [--drop-asm-nops]
+                               [--align-loops=P --loop-offset=B] [--loop-parity]
+
+What it does and why (measurements: tools/valu_runs on MI355X,
+profiles/r01s_valu_runs.jsonl, profiles/r01v_valu_runs.jsonl, and the
+scan-kernel A/Bs in profiles/r01n_e64_ab.jsonl, profiles/r01r_loop_offset_sweep.jsonl):
 
 1. VOP2 -> VOP3 encoding of full-rate integer ops (v_add_u32_e32 ->
    v_add_u32_e64, likewise lshrrev/lshlrev/xor/and/or/sub).  Same operation,
-   same result; measured on MI355X (tools/valu_runs, profiles/r01m_valu_runs.jsonl):
-   in a stream mixed with half-rate VOP3 ops (v_alignbit_b32, v_add3_u32) a
-   VOP2-encoded add/xor/shift costs ~4.1 SIMD cycles per wave instruction, the
-   VOP3-encoded one ~3.1 (and bitop3 ~3.1).  LLVM always shrinks to VOP2 when
-   it can and has no switch to keep the long form.  Only register / inline-
-   constant operands are converted (gfx950 VOP3 takes no literal).
-2. --drop-asm-nops: remove the `s_nop 0` LLVM's hazard recognizer puts after
-   an inline-asm block whose next instruction reads the block's result.  It
-   must assume the asm may be a transcendental op (1 wait state before a
-   dependent VALU on gfx940+); our blocks are single v_bitop3_b32, which LLVM
-   itself schedules back-to-back with its consumers when it emits the same
-   instruction (no wait state).
+   same result.  LLVM always shrinks to the 4-byte VOP2 form; in a stream
+   mixed with half-rate VOP3 ops (v_alignbit_b32, v_add3_u32) every 4-byte
+   instruction shifts the byte parity of the 8-byte ones that follow (2).
+   Only register / inline-constant operands are converted (gfx950 VOP3 takes
+   no literal).
+2. Byte parity of 8-byte instructions in hot loops.  A wave stream that mixes
+   half-rate VOP3 (4.3 SIMD cycles per wave instruction alone) with full-rate
+   VOP3 (2.7) issues at the additive rate only when the 8-byte instructions
+   sit at addresses = 4 (mod 8); at 0 (mod 8) EVERY instruction of the mix
+   costs ~4.2 cycles (the full-rate ones lose their advantage).  Measured on
+   the c2 scan kernel: loop start at 4 mod 8 -> 36.3 GH/s, at 0 mod 8 ->
+   32.1 GH/s, every 4-byte step of a 64-byte sweep.
+   --align-loops=3 --loop-offset=4 puts each inner-loop label at 4 (mod 8)
+   (`.p2align 3` + one `s_nop 0` executed once on loop entry).
+   --loop-parity additionally walks each inner-loop body with exact
+   instruction sizes (from llvm-mc) and restores the parity after every
+   4-byte instruction that breaks it: by widening the preceding 4-byte VALU
+   (VOP1/VOP2/VOPC e32 -> e64, same operands) where possible, else by
+   inserting one `s_nop 0` before the next 8-byte instruction.
+3. --drop-asm-nops: remove the `s_nop 0` LLVM's hazard recognizer puts after
+   an inline-asm block whose next instruction reads the block's result.  For
+   inline asm it must assume a dst_sel (16-bit) forwarding hazard on gfx950;
+   our blocks are single 32-bit v_bitop3_b32, which LLVM itself issues
+   back-to-back with its consumers when it selects the instruction.  Off by
+   default: it changes code addresses (see 2) and is not needed for speed.
 
 Prints a one-line JSON summary of what changed to stderr.
 """
 import json
+import os
 import re
+import subprocess
 import sys
+import tempfile
 
 E32_OPS = ("v_add_u32", "v_sub_u32", "v_subrev_u32", "v_lshrrev_b32", "v_lshlrev_b32", "v_xor_b32", "v_and_b32",
            "v_or_b32")
 RE_E32 = re.compile(r"^(\s*)(" + "|".join(E32_OPS) + r")_e32(\s+)(.*)$")
+# any VOP1/VOP2/VOPC in its 4-byte form (parity pass may widen it)
+RE_ANY_E32 = re.compile(r"^(\s*)(v_[a-z0-9_]+)_e32(\s+)(.*)$")
 # plain VALU consumers (no DPP/SDWA/readlane/memory): no wait state after a VALU write
 SAFE_NEXT = re.compile(r"^(v_add3_u32|v_add_u32_e(32|64)|v_alignbit_b32|v_lshrrev_b32_e(32|64)|v_xor_b32_e(32|64)|"
                        r"v_bitop3_b32|v_cndmask_b32_e(32|64))\s(?!.*(dpp|sdwa|row_|quad_))")
-REG = re.compile(r"^(v\d+|s\d+|vcc_lo|vcc_hi|exec_lo|exec_hi|m0)$")
+REG = re.compile(r"^(v\d+|s\d+|vcc_lo|vcc_hi|vcc|exec_lo|exec_hi|m0|v\[\d+:\d+\]|s\[\d+:\d+\])$")
+RE_LABEL = re.compile(r"^(\.LBB\d+_\d+):")
+RE_BRANCH = re.compile(r"^s_cbranch_\w+\s+(\.LBB\d+_\d+)")
+LLVM_MC = os.environ.get("LLVM_MC", "/opt/rocm/lib/llvm/bin/llvm-mc")
 
 
 def inline_const(tok):
@@ -41,28 +68,73 @@ def inline_const(tok):
     return -16 <= v <= 64
 
 
+def operands(text):
+    return [p.strip() for p in text.split(";")[0].split(",")]
+
+
 def convertible(ops):
-    parts = [p.strip() for p in ops.split(",")]
+    parts = operands(ops)
     if len(parts) != 3:
         return False
     return all(REG.match(p) or inline_const(p) for p in parts)
 
 
-def main():
-    src, dst = sys.argv[1], sys.argv[2]
-    e64 = "--no-e64" not in sys.argv
-    drop_nops = "--drop-asm-nops" in sys.argv
-    align = 0
-    offset = 0
-    for a in sys.argv:
-        if a.startswith("--align-loops="):
-            align = int(a.split("=")[1])
-        if a.startswith("--loop-offset="):
-            offset = int(a.split("=")[1])
-    lines = open(src).read().split("\n")
+def widen(line):
+    """4-byte VOP1/VOP2/VOPC line -> the same instruction in its 8-byte VOP3
+    form, or None when that form cannot hold the operands."""
+    m = RE_ANY_E32.match(line)
+    if not m or "dpp" in line or "sdwa" in line:
+        return None
+    parts = operands(m.group(4))
+    if not all(REG.match(p) or inline_const(p) for p in parts):
+        return None
+    return f"{m.group(1)}{m.group(2)}_e64{m.group(3)}{m.group(4)}"
+
+
+def is_instr(s):
+    return bool(s) and not s.startswith((";", ".")) and not RE_LABEL.match(s)
+
+
+def sizes_of(instrs, cpu="gfx950"):
+    """Encoded size in bytes of each instruction line (one llvm-mc run)."""
+    if not instrs:
+        return []
+    with tempfile.NamedTemporaryFile("w", suffix=".s", delete=False) as f:
+        f.write("\n".join(instrs) + "\n")
+        path = f.name
+    try:
+        r = subprocess.run([LLVM_MC, "-arch=amdgcn", f"-mcpu={cpu}", "-show-encoding", path],
+                           capture_output=True, text=True)
+    finally:
+        os.unlink(path)
+    enc = [ln for ln in r.stdout.split("\n") if "; encoding: [" in ln]
+    if len(enc) != len(instrs):
+        raise SystemExit(f"isa_post: llvm-mc sized {len(enc)} of {len(instrs)} instructions:\n{r.stderr[-2000:]}")
+    return [len(e.split("; encoding: [")[1].rstrip("]").split(",")) for e in enc]
+
+
+def loop_headers(lines):
+    """Indices of inner-loop header labels (LLVM's loop comments)."""
+    hdr = []
+    for i, ln in enumerate(lines):
+        if not RE_LABEL.match(ln):
+            continue
+        if "Inner Loop Header" in ln:
+            hdr.append(i)
+            continue
+        for ln2 in lines[i + 1:]:
+            t = ln2.strip()
+            if t and not t.startswith(";"):
+                break
+            if "Inner Loop Header" in t:
+                hdr.append(i)
+                break
+    return hdr
+
+
+def pass_encode(lines, e64, drop_nops, stats):
     out = []
-    n_e64 = n_nop = 0
-    last_asm_bitop3 = False  # previous real instruction came from a v_bitop3 inline-asm block
+    last_asm_bitop3 = False
     in_asm = False
 
     def next_real(i):
@@ -73,51 +145,98 @@ def main():
             return t
         return ""
 
-    def is_loop_header(i):
-        # the label line and the comment-only lines that follow it
-        if "Inner Loop Header" in lines[i]:
-            return True
-        for ln2 in lines[i + 1:]:
-            t = ln2.strip()
-            if t and not t.startswith(";"):
-                return False
-            if "Inner Loop Header" in t:
-                return True
-        return False
-
-    n_align = 0
     for i, ln in enumerate(lines):
         s = ln.strip()
-        if align and re.match(r"^\.LBB\d+_\d+:", ln) and is_loop_header(i):
-            out.append(f"\t.p2align {align}")
-            out += ["\ts_nop 0"] * (offset // 4)
-            n_align += 1
         if s == ";;#ASMSTART":
             in_asm = True
-            out.append(ln)
-            continue
-        if s == ";;#ASMEND":
+        elif s == ";;#ASMEND":
             in_asm = False
-            out.append(ln)
-            continue
-        if not s or s.startswith(";"):
-            out.append(ln)
-            continue
-        if in_asm:
-            last_asm_bitop3 = s.startswith("v_bitop3_b32")
-            out.append(ln)
-            continue
-        if drop_nops and last_asm_bitop3 and s == "s_nop 0" and SAFE_NEXT.match(next_real(i)):
-            n_nop += 1
-            continue
-        last_asm_bitop3 = False
-        m = RE_E32.match(ln)
-        if e64 and m and convertible(m.group(4).split(";")[0]):
-            ln = f"{m.group(1)}{m.group(2)}_e64{m.group(3)}{m.group(4)}"
-            n_e64 += 1
+        elif s and not s.startswith(";"):
+            if in_asm:
+                last_asm_bitop3 = s.startswith("v_bitop3_b32")
+            elif drop_nops and last_asm_bitop3 and s == "s_nop 0" and SAFE_NEXT.match(next_real(i)):
+                stats["asm_nops_dropped"] += 1
+                continue
+            else:
+                last_asm_bitop3 = False
+                m = RE_E32.match(ln)
+                if e64 and m and convertible(m.group(4)):
+                    ln = f"{m.group(1)}{m.group(2)}_e64{m.group(3)}{m.group(4)}"
+                    stats["e64_converted"] += 1
         out.append(ln)
-    open(dst, "w").write("\n".join(out))
-    print(json.dumps({"e64_converted": n_e64, "asm_nops_dropped": n_nop, "loops_aligned": n_align}), file=sys.stderr)
+    return out
+
+
+def pass_align(lines, align, offset, stats):
+    hdr = set(loop_headers(lines))
+    out = []
+    for i, ln in enumerate(lines):
+        if i in hdr:
+            out.append(f"\t.p2align {align}")
+            out += ["\ts_nop 0"] * (offset // 4)
+            stats["loops_aligned"] += 1
+        out.append(ln)
+    return out
+
+
+def pass_parity(lines, stats):
+    """Inner-loop bodies (label .. branch back to it) start at 4 mod 8 (pass_align
+    with offset 4); keep every 8-byte instruction in them at 4 mod 8."""
+    regions = []
+    for h in loop_headers(lines):
+        label = RE_LABEL.match(lines[h]).group(1)
+        for j in range(h + 1, min(len(lines), h + 40000)):
+            m = RE_BRANCH.match(lines[j].strip())
+            if m and m.group(1) == label:
+                regions.append((h, j))
+                break
+    body_idx = [k for a, b in regions for k in range(a + 1, b + 1) if is_instr(lines[k].strip())]
+    size = dict(zip(body_idx, sizes_of([lines[k].strip() for k in body_idx])))
+    in_region = {}
+    for a, b in regions:
+        for k in range(a + 1, b + 1):
+            in_region[k] = a
+    out = []
+    pos = None
+    last_small = None  # index in `out` of the last 4-byte instruction since the last 8-byte one
+    for i, ln in enumerate(lines):
+        if i in in_region and i == in_region[i] + 1:
+            pos, last_small = 4, None
+        if i not in in_region or i not in size:
+            out.append(ln)
+            continue
+        sz = size[i]
+        if sz == 8 and pos % 8 == 0:
+            w = widen(out[last_small]) if last_small is not None else None
+            if w is not None:
+                out[last_small] = w
+                stats["parity_widened"] += 1
+            else:
+                out.append("\ts_nop 0")
+                stats["parity_nops"] += 1
+            pos += 4
+        out.append(ln)
+        pos += sz
+        last_small = len(out) - 1 if sz == 4 and ln.strip().startswith("v_") else (
+            last_small if sz == 4 else None)
+    return out
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    args = sys.argv[3:]
+    opt = {a.split("=")[0]: (a.split("=")[1] if "=" in a else True) for a in args}
+    stats = {"e64_converted": 0, "asm_nops_dropped": 0, "loops_aligned": 0, "parity_widened": 0, "parity_nops": 0}
+    lines = open(src).read().split("\n")
+    lines = pass_encode(lines, "--no-e64" not in opt, "--drop-asm-nops" in opt, stats)
+    if "--align-loops" in opt:
+        lines = pass_align(lines, int(opt["--align-loops"]), int(opt.get("--loop-offset", 0)), stats)
+    if "--loop-parity" in opt:
+        if opt.get("--align-loops") != "3" or opt.get("--loop-offset") != "4":
+            raise SystemExit("--loop-parity needs --align-loops=3 --loop-offset=4")
+        lines = pass_parity(lines, stats)
+    open(dst, "w").write("\n".join(lines))
+    print(json.dumps(stats), file=sys.stderr)
 
 
 if __name__ == "__main__":
