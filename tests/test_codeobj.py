@@ -48,15 +48,6 @@ def test_code_object_is_gfx950_with_all_kernels(codeobj):
         assert f"{k}.kd" in hdr
 
 
-def test_no_scalar_stores(codeobj):
-    """Nothing writes through the scalar data cache (pool rule)."""
-    dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", codeobj], capture_output=True, text=True,
-                         check=True).stdout
-    bad = re.findall(r"\b(s_store_dword\w*|s_buffer_store\w*|s_scratch_store\w*|s_dcache_wb\w*|s_dcache_discard\w*|"
-                     r"s_atomic\w*|s_buffer_atomic\w*)\b", dis)
-    assert not bad, sorted(set(bad))
-
-
 def test_hot_loops_keep_4_mod_8_parity(codeobj):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_parity.py"), codeobj],
                        capture_output=True, text=True, check=True)

@@ -18,6 +18,22 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def workload_stats(trace, out):
+    """rocprofv3 --kernel-trace rows of the workload's k_scan launches only
+    (largest grid; bench.py's configs[0]-sized latency probe launches small
+    grids of the same kernel), in the --stats CSV layout."""
+    rows = [r for r in csv.DictReader(open(trace)) if r["Kernel_Name"].startswith("k_scan")]
+    if not rows:
+        return
+    g = max(int(r["Grid_Size_X"]) for r in rows)
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if int(r["Grid_Size_X"]) == g]
+    mean = sum(d) / len(d)
+    sd = (sum((x - mean) ** 2 for x in d) / len(d)) ** 0.5
+    with open(out, "w") as f:
+        f.write('"Name","Calls","TotalDurationNs","AverageNs","MinNs","MaxNs","StdDev","Grid_Size_X","Source"\n')
+        f.write(f'"k_scan",{len(d)},{sum(d)},{mean:.1f},{min(d)},{max(d)},{sd:.1f},{g},"{os.path.basename(trace)}"\n')
+
+
 def main():
     tag = sys.argv[1]
     nonces = float(sys.argv[2]) if len(sys.argv) > 2 else 2.0**32
@@ -27,6 +43,9 @@ def main():
     ks = os.path.join(src, f"{tag}_prof", "run_kernel_stats.csv")
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    kt = os.path.join(src, f"{tag}_prof", "run_kernel_trace.csv")
+    if os.path.exists(kt):
+        workload_stats(kt, os.path.join(dst, f"{tag}_kernel_stats_workload.csv"))
     for f in glob.glob(os.path.join(src, f"{tag}_bench*.json")) + glob.glob(os.path.join(src, f"{tag}_valu_*.jsonl")):
         shutil.copy(f, os.path.join(dst, os.path.basename(f)))
     counters, durs = {}, []
