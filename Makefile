@@ -40,11 +40,14 @@ p1_amd/libp1hip.so: $(BUILD)/p1hip_host.o $(BUILD)/p1hip_kernels_blob.o
 	$(HIPCC) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 # C++ host mirror of the reference's bitcoin package + miner loop (stdio)
-p1_amd/p1miner: p1_amd/host/p1miner.cpp p1_amd/host/bitcoin.cpp p1_amd/host/bitcoin.hpp include/p1hip.h p1_amd/libp1hip.so
-	g++ -O2 -std=c++17 -Wall -Wextra -o $@ p1_amd/host/p1miner.cpp p1_amd/host/bitcoin.cpp -Lp1_amd -lp1hip -Wl,-rpath,'$$ORIGIN'
+HOSTSRC := p1_amd/host/bitcoin.cpp p1_amd/host/lsp_message.cpp
+HOSTHDR := p1_amd/host/bitcoin.hpp p1_amd/host/lsp_message.hpp p1_amd/host/gojson.hpp include/p1hip.h
 
-p1_amd/p1server: p1_amd/host/p1server.cpp p1_amd/host/bitcoin.cpp p1_amd/host/bitcoin.hpp include/p1hip.h p1_amd/libp1hip.so
-	g++ -O2 -std=c++17 -Wall -Wextra -o $@ p1_amd/host/p1server.cpp p1_amd/host/bitcoin.cpp -Lp1_amd -lp1hip -Wl,-rpath,'$$ORIGIN'
+p1_amd/p1miner: p1_amd/host/p1miner.cpp $(HOSTSRC) $(HOSTHDR) p1_amd/libp1hip.so
+	g++ -O2 -std=c++17 -Wall -Wextra -o $@ p1_amd/host/p1miner.cpp $(HOSTSRC) -Lp1_amd -lp1hip -Wl,-rpath,'$$ORIGIN'
+
+p1_amd/p1server: p1_amd/host/p1server.cpp $(HOSTSRC) $(HOSTHDR) p1_amd/libp1hip.so
+	g++ -O2 -std=c++17 -Wall -Wextra -o $@ p1_amd/host/p1server.cpp $(HOSTSRC) -Lp1_amd -lp1hip -Wl,-rpath,'$$ORIGIN'
 
 # host-only replay of the kernels' per-thread code (layout tests; not product)
 tools/p1emu: tools/p1emu.cpp $(HDRS)

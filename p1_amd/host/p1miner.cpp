@@ -12,6 +12,13 @@
 //                                        Result line (Join/Result lines ignored)
 //   p1miner json                         re-marshals stdin JSON lines (no GPU;
 //                                        wire-format tests)
+//   p1miner lsp-json                     re-marshals stdin lsp.Message JSON lines
+//                                        (lsp/message.go; no GPU)
+//   p1miner lsp-wrap <connID> <seq>      each stdin bitcoin.Message JSON line ->
+//                                        the LSP Data datagram that carries it
+//                                        (miner.go:66 client.Write), seq counting up
+//   p1miner lsp-unwrap                   LSP Data datagram lines -> the bitcoin
+//                                        message in their payload (miner.go:50-55)
 #include <errno.h>
 #include <inttypes.h>
 #include <stdio.h>
@@ -23,11 +30,12 @@
 
 #include "../../include/p1hip.h"
 #include "bitcoin.hpp"
+#include "lsp_message.hpp"
 
 static int usage() {
   fprintf(stderr,
           "usage: p1miner scan <msg> <lower> <upper> | hash <msg> <nonce> | "
-          "serve [--device N] [--chunk C] | json\n");
+          "serve [--device N] [--chunk C] | json | lsp-json | lsp-wrap <connID> <seq> | lsp-unwrap\n");
   return 2;
 }
 
@@ -64,6 +72,44 @@ int main(int argc, char** argv) {
         bitcoin::Message m;
         if (!bitcoin::Unmarshal(line, &m)) { printf("ERROR\n"); continue; }
         printf("%s\t%s\n", bitcoin::Marshal(m).c_str(), m.String().c_str());
+      }
+      return 0;
+    }
+    if (cmd == "lsp-json") {
+      std::string line;
+      while (std::getline(std::cin, line)) {
+        lsp::Message m;
+        if (!lsp::Unmarshal(line, &m)) { printf("ERROR\n"); continue; }
+        printf("%s\t%s\n", lsp::Marshal(m).c_str(), m.String().c_str());
+      }
+      return 0;
+    }
+    if (cmd == "lsp-wrap" && argc == 4) {
+      char* end = nullptr;
+      const long long conn = strtoll(argv[2], &end, 10);
+      if (*end) return usage();
+      long long seq = strtoll(argv[3], &end, 10);
+      if (*end) return usage();
+      std::string line;
+      while (std::getline(std::cin, line)) {
+        bitcoin::Message m;
+        if (!bitcoin::Unmarshal(line, &m)) { printf("ERROR\n"); continue; }
+        const std::string payload = bitcoin::Marshal(m);
+        printf("%s\n", lsp::Marshal(lsp::NewData(conn, seq++, (int64_t)payload.size(), payload)).c_str());
+      }
+      return 0;
+    }
+    if (cmd == "lsp-unwrap") {
+      std::string line;
+      while (std::getline(std::cin, line)) {
+        lsp::Message d;
+        bitcoin::Message m;
+        if (!lsp::Unmarshal(line, &d) || d.Type != lsp::MsgData ||
+            !bitcoin::Unmarshal(std::string(d.Payload.begin(), d.Payload.end()), &m)) {
+          printf("ERROR\n");
+          continue;
+        }
+        printf("%s\n", bitcoin::Marshal(m).c_str());
       }
       return 0;
     }

@@ -80,3 +80,47 @@ def test_cli_serve_loop(oracle_mod):
     want = [oracle_mod.scan(q["Data"], q["Lower"], q["Upper"], threads=8) for q in reqs[1:]]
     assert [(x["Hash"], x["Nonce"]) for x in res] == want
     assert want[-1] == (U64_MAX, 0)
+
+
+def test_lsp_message_wire_format_matches_go():
+    # Go encoding/json of lsp.Message (lsp/message.go:16-22): Type, ConnID,
+    # SeqNum, Size, Payload ([]byte as padded standard base64, nil as null).
+    # Line 1 is the Connect datagram of SURVEY.md Appendix B (what mtest's
+    # server accepts); String() follows message.go:51-62.
+    lines = [
+        '{"Type":0,"ConnID":0,"SeqNum":0,"Size":0,"Payload":null}',
+        '{"Type":1,"ConnID":3,"SeqNum":1,"Size":5,"Payload":"aGVsbG8="}',
+        '{"type":2,"connid":3,"seqnum":1}',                       # case-insensitive keys, missing fields
+        '{"Type":1,"ConnID":1,"SeqNum":2,"Size":0,"Payload":""}',  # empty, non-nil slice
+        '{"Type":1,"Payload":"aGVsbG8"}',                          # unpadded base64: Go rejects it
+        '{"Type":1,"SeqNum":1.5}',                                 # not an int
+        '{"Type":1,"ConnID":-9223372036854775808,"SeqNum":9223372036854775807,"Payload":"w6k="}',
+        '{"Type":1,"ConnID":9223372036854775808}',                 # int64 overflow
+    ]
+    out = run(["lsp-json"], "\n".join(lines) + "\n").stdout.split("\n")
+    assert out[0] == lines[0] + "\t[Connect 0 0]"
+    assert out[1] == lines[1] + "\t[Data 3 1 hello]"
+    assert out[2] == '{"Type":2,"ConnID":3,"SeqNum":1,"Size":0,"Payload":null}\t[Ack 3 1]'
+    assert out[3] == lines[3] + "\t[Data 1 2 ]"
+    assert out[4] == "ERROR" and out[5] == "ERROR" and out[7] == "ERROR"
+    assert out[6].split("\t")[0] == \
+        '{"Type":1,"ConnID":-9223372036854775808,"SeqNum":9223372036854775807,"Size":0,"Payload":"w6k="}'
+
+
+def test_lsp_framing_of_bitcoin_messages():
+    # miner.go:21,66: client.Write(json.Marshal(msg)) -> one LSP Data datagram
+    # whose Payload is the bitcoin.Message JSON and Size its length.
+    import base64
+
+    msgs = ['{"Type":0,"Data":"","Lower":0,"Upper":0,"Hash":0,"Nonce":0}',
+            '{"Type":2,"Data":"","Lower":0,"Upper":0,"Hash":1419516646206828,"Nonce":9898}',
+            '{"Type":1,"Data":"~~~???","Lower":7,"Upper":8,"Hash":0,"Nonce":0}']  # '+' and '/' in base64
+    wrapped = run(["lsp-wrap", "7", "1"], "\n".join(msgs) + "\n").stdout.strip().split("\n")
+    for i, (w, m) in enumerate(zip(wrapped, msgs)):
+        d = json.loads(w)
+        assert list(d) == ["Type", "ConnID", "SeqNum", "Size", "Payload"]
+        assert (d["Type"], d["ConnID"], d["SeqNum"], d["Size"]) == (1, 7, 1 + i, len(m))
+        assert base64.b64decode(d["Payload"]).decode() == m
+    assert "+" in wrapped[2] and "/" in wrapped[2]
+    back = run(["lsp-unwrap"], "\n".join(wrapped) + "\n").stdout.strip().split("\n")
+    assert back == msgs
