@@ -4,22 +4,33 @@
 Metric (BASELINE.json): SHA-256 nonce-hashes/s (GH/s) at 1/2/4/8 MI355X and
 the fraction of the integer-VALU roofline.
 
-Workload (BASELINE.json configs[1], "c2"): msg = "bradfitz" (8 bytes), the
-nonce range [0, 2^32) per GPU -- one SHA-256 compression per nonce.  A step
-is one full scan of that range (the drop-in for miner.go:56-63) ending with
-the (hash, nonce) result on the host.  With N GPUs (torchrun, one process per
-GPU) the job range is [0, N*2^32), sharded contiguously (weak scaling); the
-16-byte per-rank results are all-gathered over RCCL (torch.distributed
-"nccl") and reduced with the lexicographic (hash, nonce) min.  `--config c3`
-selects configs[2] (120-byte msg, 2^34 nonces per GPU, 2 tail blocks);
-`--config c4` selects configs[3] (the fixed [0, 2^38) job split over the GPUs,
-strong scaling).
+Workloads (BASELINE.json configs):
+  c2  configs[1]: msg "bradfitz" (8 B), nonces [0, 2^32) per GPU, one SHA-256
+      compression per nonce.  The default at N = 1 (the metric's config).
+  c3  configs[2]: 120-byte msg (host midstate), [0, 2^34) per GPU, 2 tail blocks.
+  c4  configs[3]: msg "bradfitz", the FIXED job [0, 2^38) split contiguously
+      over the N GPUs (strong scaling).  The default at N > 1: north_star's
+      scaling target is stated on this range.
+A step is one full scan of the job (the drop-in for miner.go:56-63) ending
+with the (hash, nonce) result on the host.
+
+How N GPUs are driven:
+  * torchrun (WORLD_SIZE > 1, the driver's launch): one process per GPU; each
+    rank scans one contiguous shard through the library and the 16-byte
+    results are all-gathered over torch.distributed "nccl" (RCCL over xGMI).
+  * `python bench.py --gpus N` without torchrun: ONE process opens N devices
+    through the library itself (p1hip_init(N): one host thread per device,
+    ncclCommInitAll, ncclAllGather of the 16-byte partials inside p1hip_scan).
+  * --gpus larger than the visible device count exits non-zero; it never
+    silently falls back to fewer GPUs.
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import glob
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -36,6 +47,9 @@ VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
 # alignbit/add3 (profiles/r01_valu_peak.jsonl), so it is reported beside.
 SURVEY_PEAK_OPS = 39.32e12
 ALG_OPS_PER_COMPRESSION = 1384  # 64 rounds x 14 + 48 schedule words x 10 + 8
+# The reference's own published rate for bitcoin.Hash: "around 10,000 per
+# second" on a typical Andrew Linux machine (p1.pdf 4.1).
+PUBLISHED_HASHES_PER_S = 1.0e4
 
 CONFIGS = {
     "c2": {"msg": b"bradfitz", "per_gpu": 1 << 32, "b_tail": 1,
@@ -47,7 +61,8 @@ CONFIGS = {
     # configs[3]: the fixed 2^38 job split over however many GPUs run (strong scaling)
     "c4": {"msg": b"bradfitz", "total": 1 << 38, "b_tail": 1,
            "desc": "configs[3]: 8-byte msg 'bradfitz', nonces [0,2^38) split contiguously over the GPUs",
-           "known": {}},
+           # the same job whatever N is: profiles/r02a_c4.json (1 GPU)
+           "known_any": (52863133, 182986939864)},
 }
 
 
@@ -57,6 +72,44 @@ CONFIGS = {
 ALG_MIX = {"v_alignbit_b32": 576, "v_bitop3_b32": 352, "v_add3_u32": 240, "v_add_u32": 120,
            "v_lshrrev_b32": 96}
 VALU_PEAK_PROFILE = "profiles/r01_valu_peak.jsonl"
+
+
+class UsageError(SystemExit):
+    pass
+
+
+def resolve_run(gpus, config, env, visible):
+    """How this invocation uses the GPUs.
+
+    Returns a dict: mode ("single" | "library" | "torchrun"), n (GPUs in the
+    job), rank, world (processes), local_rank, config.  Raises UsageError
+    (non-zero exit) when the request cannot be honoured -- never falls back to
+    fewer GPUs than asked for."""
+    world = int(env.get("WORLD_SIZE", "1") or 1)
+    rank = int(env.get("RANK", "0") or 0)
+    local = int(env.get("LOCAL_RANK", "0") or 0)
+    if gpus < 1:
+        raise UsageError(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    if world > 1:
+        if gpus != world:
+            raise UsageError(f"bench.py: --gpus {gpus} but torchrun started {world} ranks (WORLD_SIZE)")
+        mode, n = "torchrun", world
+    else:
+        if gpus > visible:
+            raise UsageError(f"bench.py: --gpus {gpus} but only {visible} GPU(s) are visible")
+        mode, n = ("library" if gpus > 1 else "single"), gpus
+    cfg = config or ("c2" if n == 1 else "c4")
+    return {"mode": mode, "n": n, "rank": rank, "world": world, "local_rank": local, "config": cfg}
+
+
+def job_total(cfg, n):
+    return cfg["total"] if "total" in cfg else cfg["per_gpu"] * n
+
+
+def known_answer(cfg, n):
+    if "known_any" in cfg:
+        return cfg["known_any"]
+    return cfg["known"].get(n)
 
 
 def mix_roofline():
@@ -83,42 +136,75 @@ def mix_roofline():
             "rates_lane_ops_per_clk_cu": rate, "source": VALU_PEAK_PROFILE}
 
 
-def pmc_traffic():
-    """HBM bytes per k_scan launch from the newest committed rocprofv3 PMC
-    summary (profiles/*_pmc_summary.json, FETCH_SIZE + WRITE_SIZE of the c2
-    workload, collected in separate --pmc passes by tools/gpu_round.sh)."""
-    import glob
+def pmc_summary(config):
+    """Newest committed rocprofv3 PMC summary of this config's k_scan launch
+    (profiles/*_pmc_summary.json written by tools/summarize_prof.py; the
+    counters come from separate --pmc passes of the same bench command)."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("config", "c2") == config:
+            best = (d, os.path.relpath(p, ROOT))
+    return best if best else (None, None)
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+def host_cores():
+    """CPU cores this process may run on: the affinity mask, capped by the
+    cgroup CPU quota when one is set (a GPU box shares its host)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return (min(n, quota) if quota else n), n, quota, model
 
 
-def cpu_baseline(msg, start, target_s):
+def cpu_baseline(msg, start, target_s, runs=5):
     """Oracle restatement (format + full SHA-256 per nonce, the reference's
-    per-nonce work) on the host cores, bounded sample."""
+    per-nonce work) on every host core this process may use, contiguous
+    sub-ranges per thread (the reference's goroutine-per-core plan,
+    BASELINE.md 4); median of `runs` timed runs over a bounded sample."""
     import oracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
-    cal = 1 << 18
+    threads, affinity, quota, model = host_cores()
+    cal = 1 << 16
     t0 = time.perf_counter()
     oracle.scan(msg, start, start + cal * threads - 1, threads=threads)
     rate = cal * threads / (time.perf_counter() - t0)
-    n = max(int(rate * target_s), cal * threads)
-    t0 = time.perf_counter()
-    oracle.scan(msg, start, start + n - 1, threads=threads)
-    dt = time.perf_counter() - t0
+    n = max(int(rate * target_s / runs), cal * threads)
+    rates = []
+    for i in range(runs):
+        lo = start + i * n
+        t0 = time.perf_counter()
+        oracle.scan(msg, lo, lo + n - 1, threads=threads)
+        rates.append(n / (time.perf_counter() - t0))
+    med = statistics.median(rates)
     return {
-        "value": n / dt / 1e9,
+        "value": med / 1e9,
         "unit": "GH/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"oracle/p1_oracle.c (C restatement of hash.go:13-17 + miner.go:56-63, sprintf-equivalent "
-                  f"formatting + full SHA-256 per nonce), {threads} threads, nonces [{start}, {start + n - 1}] "
-                  f"({n} nonces, {dt:.1f} s) of the same message",
+        "runs_GH_s": [r / 1e9 for r in rates],
+        "host": {"cpu_model": model, "affinity_cpus": affinity, "cgroup_quota_cpus": quota,
+                 "os_cpu_count": os.cpu_count()},
+        "sample": f"oracle/p1_oracle.c (C restatement of hash.go:13-17 + miner.go:56-63: %d formatting + "
+                  f"full SHA-256 per nonce; not the Go reference, which cannot be built here), {threads} "
+                  f"threads over contiguous sub-ranges, median of {runs} runs of {n} nonces each starting "
+                  f"at nonce {start} of the same message",
     }
 
 
@@ -127,23 +213,30 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="default: c2 at one GPU, c4 (fixed [0,2^38) job) at N > 1")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-small-request", action="store_true",
                     help="skip the configs[0]-sized latency probe (profiling runs: keeps every "
                          "k_scan launch in the rocprof summary a workload launch)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="nccl = RCCL over xGMI (production); gloo only to rehearse "
+                    help="torchrun path: nccl = RCCL over xGMI (production); gloo only to rehearse "
                          "several ranks on one GPU")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
-    cfg = CONFIGS[args.config]
-
     import torch
+
+    visible = torch.cuda.device_count()
+    try:
+        run = resolve_run(args.gpus, args.config, os.environ,
+                          visible if args.dist_backend == "nccl" else max(visible, args.gpus))
+    except UsageError as e:
+        print(str(e), file=sys.stderr)
+        sys.exit(2)
+    cfg = CONFIGS[run["config"]]
+    mode, n_gpus, rank, world = run["mode"], run["n"], run["rank"], run["world"]
+
     import torch.distributed as dist
 
     import p1_amd
@@ -152,31 +245,37 @@ def main():
 
     ensure_built()
 
-    ngpu = torch.cuda.device_count()
-    gpu = local % ngpu if args.dist_backend == "gloo" else local  # gloo rehearsal may share a GPU
-    if world > 1:
+    msg = cfg["msg"]
+    total = job_total(cfg, n_gpus)
+    if mode == "torchrun":
+        gpu = run["local_rank"] % visible if args.dist_backend == "gloo" else run["local_rank"]
         torch.cuda.set_device(gpu)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group("gloo")
-    p1_amd.init_devices([gpu])
-
-    msg = cfg["msg"]
-    total = cfg["total"] if "total" in cfg else cfg["per_gpu"] * world
-    shard = p1_amd.shard_range(0, total - 1, rank, world)
-    dev = torch.device("cuda", gpu)
-    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+        p1_amd.init_devices([gpu])
+        devices = [gpu]
+        coll_dev = torch.device("cuda", gpu) if args.dist_backend == "nccl" else torch.device("cpu")
+        sync_devs = [gpu]
+    else:
+        got = p1_amd.init(n_gpus)
+        if got != n_gpus:
+            print(f"bench.py: library opened {got} devices, asked for {n_gpus}", file=sys.stderr)
+            sys.exit(2)
+        devices = list(range(n_gpus))
+        sync_devs = devices
 
     def step():
-        if world == 1:
-            return p1_amd.scan(msg, shard[0], shard[1])
-        return distributed_scan(msg, 0, total - 1, p1_amd.scan, device=coll_dev)
+        if mode == "torchrun":
+            return distributed_scan(msg, 0, total - 1, p1_amd.scan, device=coll_dev)
+        return p1_amd.scan(msg, 0, total - 1)  # library: shards + RCCL all-gather inside
 
     def barrier():
-        if world > 1:
+        if mode == "torchrun":
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        for d in sync_devs:
+            torch.cuda.synchronize(d)
 
     for _ in range(args.warmup):
         step()
@@ -190,71 +289,102 @@ def main():
     p1_amd.set_profiling(False)
     stats = p1_amd.get_stats()
 
-    if world > 1:
+    if mode == "torchrun":
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     result = results[-1]
     consistent = all(r == result for r in results)
-    known = cfg["known"].get(world)
+    known = known_answer(cfg, n_gpus)
 
     if rank == 0:
         hashes = total * args.steps
         value = hashes / elapsed / 1e9
         ms_per_step = elapsed * 1e3 / args.steps
-        traffic, traffic_src = pmc_traffic() if args.config == "c2" else (None, None)
-        k_ms = stats["scan_kernel_ms"]
+        k_ms = stats["scan_kernel_ms"]  # summed over this process's devices
         k_n = stats["scan_launches"]
+        # one launch = one device's k_scan; its algorithmic ops / its own duration
         achieved = stats["scan_alg_ops"] / (k_ms * 1e-3) if k_ms > 0 else 0.0
+        k_rate = stats["scan_nonces"] / (k_ms * 1e-3) if k_ms > 0 else 0.0  # nonces/s per device
+        pmc, pmc_src = pmc_summary(run["config"])
         roofline = {
             "bound": "valu-int32",
             "achieved": achieved / 1e12,
             "peak": VALU_PEAK_OPS / 1e12,
             "unit": "TOP/s",
             "frac": achieved / VALU_PEAK_OPS,
-            "traffic": traffic,
+            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
             "traffic_unit": "bytes/launch (PMC FETCH_SIZE+WRITE_SIZE)",
-            "traffic_source": traffic_src,
+            "traffic_source": pmc_src,
             "kernel": "k_scan (one launch per scan covers every decade; algorithmic ops = 1384 x B_tail per nonce)",
             "alg_ops_per_nonce": ALG_OPS_PER_COMPRESSION * cfg["b_tail"],
             "avg_launch_ms": k_ms / k_n if k_n else None,
             "launches_per_step": k_n / args.steps,
-            "kernel_hashes_per_s_G": stats["scan_nonces"] / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None,
+            "kernel_hashes_per_s_G": k_rate / 1e9,
             "frac_vs_survey_peak": achieved / SURVEY_PEAK_OPS,
             "fast_nonce_share": stats["fast_nonces"] / max(1, stats["fast_nonces"] + stats["generic_nonces"]),
         }
+        if pmc and pmc.get("valu_wave_instr_per_nonce"):
+            # SURVEY.md 8(d) accounting rule: beside the algorithmic fraction,
+            # the executed-instruction fraction SQ_INSTS_VALU x 64 / (t x peak),
+            # with this run's kernel rate and the PMC instructions per nonce
+            ipn = pmc["valu_wave_instr_per_nonce"]
+            roofline["executed"] = {
+                "valu_instr_per_nonce": ipn,
+                "achieved": ipn * k_rate / 1e12,
+                "frac": ipn * k_rate / VALU_PEAK_OPS,
+                "issue_frac": pmc.get("issue_frac"),
+                "simd_cycles_per_valu_wave_instr": pmc.get("simd_cycles_per_valu_wave_instr"),
+                "valu_busy_frac": pmc.get("valu_busy_frac"),
+                "source": pmc_src,
+                "note": "frac counts executed VALU lane-instructions against the same 78.6 T peak; "
+                        "issue_frac prices the executed mix at the measured per-class issue costs "
+                        "(half-rate alignbit/add3 vs full-rate ops, DESIGN.md 4)",
+            }
+            if roofline["frac"] > 1.0:
+                roofline["executed"]["why_alg_frac_above_1"] = (
+                    "the algorithmic count charges both tail blocks per nonce (SURVEY.md 8(d)); the kernel "
+                    "computes the hi-digit block once per 10^3 nonces (PRE) and executes ~1 block per nonce")
         mix = mix_roofline()
         if mix and k_ms > 0:
-            khs = stats["scan_nonces"] / (k_ms * 1e-3) / 1e9
             mix["peak_GH_s"] = mix["peak_GH_s_per_block"] / cfg["b_tail"]
-            mix["frac"] = khs / mix["peak_GH_s"]
+            mix["frac"] = k_rate / 1e9 / mix["peak_GH_s"]
             roofline["mix_roofline"] = mix
+        parallelism = {"single": "1 GPU",
+                       "library": f"range-shard x{n_gpus}, one process (p1hip_init({n_gpus}): thread per device, "
+                                  f"ncclCommInitAll + ncclAllGather of 16-B partials)",
+                       "torchrun": f"range-shard x{n_gpus}, one process per GPU + "
+                                   + ("RCCL all-gather (torch.distributed nccl)" if args.dist_backend == "nccl"
+                                      else "gloo all-gather (rehearsal)")}[mode]
         line = {
             "metric": "SHA-256 nonce-hashes/sec (GH/s)",
             "value": value,
             "unit": "GH/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "strong" if "total" in cfg else "weak",
-            "vs_baseline": None,
+            "vs_baseline": value * 1e9 / PUBLISHED_HASHES_PER_S,
+            "vs_baseline_basis": "value / the reference's published bitcoin.Hash rate, 'around 10,000 per "
+                                 "second' (p1.pdf 4.1, BASELINE.md 1)",
             "dtype": "u32",
             "data": "synthetic",
             "config": {
                 "workload": cfg["desc"],
+                "config": run["config"],
                 "msg_len": len(msg),
-                "nonces_per_gpu": total // world,
+                "nonces_per_gpu": total // n_gpus,
                 "job_range": [0, total - 1],
-                "parallelism": f"range-shard x{world}" + (
-                    (" + RCCL all-gather" if args.dist_backend == "nccl" else " + gloo all-gather (rehearsal)")
-                    if world > 1 else ""),
+                "parallelism": parallelism,
+                "launch": mode,
+                "devices": devices if mode != "torchrun" else f"one per rank, {world} ranks",
             },
             "roofline": roofline,
             "result": {"hash": result[0], "nonce": result[1], "consistent": consistent,
-                       "matches_known": (tuple(result) == known) if known else None},
+                       "matches_known": (tuple(result) == tuple(known)) if known else None},
         }
         # configs[0]'s request (client 'bradfitz' maxNonce 9999) as one
         # drop-in call: per-request latency of p1hip_scan on a small job
@@ -268,13 +398,15 @@ def main():
             line["small_request"] = {"request": "bradfitz [0, 9999] (configs[0])", "result": list(small),
                                      "matches_known": tuple(small) == (1419516646206828, 9898),
                                      "median_latency_us": lat[len(lat) // 2] * 1e6}
-        if world == 1 and not args.no_cpu:
+        if n_gpus == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(msg, 1 << 31, args.cpu_seconds)
         print(json.dumps(line), flush=True)
 
-    if world > 1:
+    if mode == "torchrun":
         dist.destroy_process_group()
     p1_amd.shutdown()
+    if known and tuple(result) != tuple(known):
+        sys.exit(3)  # a wrong answer is not a benchmark result
 
 
 if __name__ == "__main__":

@@ -99,7 +99,16 @@ struct Runtime {
   std::mutex mu;
   std::vector<Dev> devs;
   bool profiling = false;
-  bool use_rccl = true;
+  bool use_rccl = true;   // multi-device combine through ncclAllGather
+  bool rccl_one = false;  // P1HIP_FORCE_RCCL=1: communicator even for one device
+  // Test-only knobs, read from the environment at init (never set in
+  // production; see tests/test_gpu_parity.py):
+  //   P1HIP_MIN_FAST_THREADS  planner occupancy floor (1 keeps k = 3 on small
+  //                           ranges so every k = 3 variant runs on the GPU)
+  //   P1HIP_TEST_FAIL_DEVICE  device index whose scan phase reports a failure
+  //                           (exercises the multi-device error path)
+  uint64_t min_fast_threads = kMinFastThreads;
+  int fail_device = -1;
   p1hip_stats_t stats{};
 };
 
@@ -181,7 +190,13 @@ int init_devs(Runtime& R, const std::vector<int>& ords) {
   // combine) can be exercised with the same GPU listed twice on a 1-GPU box.
   const char* norccl = getenv("P1HIP_NO_RCCL");
   R.use_rccl = !(norccl && norccl[0] == '1');
-  if (nd > 1 && R.use_rccl) {
+  const char* force = getenv("P1HIP_FORCE_RCCL");
+  R.rccl_one = force && force[0] == '1' && R.use_rccl;
+  const char* mft = getenv("P1HIP_MIN_FAST_THREADS");
+  R.min_fast_threads = mft && *mft ? strtoull(mft, nullptr, 10) : kMinFastThreads;
+  const char* fdev = getenv("P1HIP_TEST_FAIL_DEVICE");
+  R.fail_device = fdev && *fdev ? atoi(fdev) : -1;
+  if ((nd > 1 || R.rccl_one) && R.use_rccl) {
     std::vector<ncclComm_t> comms(nd);
     NCCLCHK(ncclCommInitAll(comms.data(), nd, ords.data()));
     for (int i = 0; i < nd; ++i) R.devs[i].comm = comms[i];
@@ -207,13 +222,14 @@ int ensure_init(Runtime& R) {
 }
 
 // Run one device's share [lo, hi] (lo <= hi) and leave its Key in d.d_res.
-int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, bool profiling) {
+int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, bool profiling,
+              uint64_t min_fast_threads) {
   HIPCHK(hipSetDevice(d.ordinal));
   d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
   d.scan_launches = d.scan_nonces = d.scan_ops = 0;
   d.fast_ms = d.scan_ms = 0.0;
   Plan plan;
-  std::string err = make_plan(msg, len, lo, hi, plan);
+  std::string err = make_plan(msg, len, lo, hi, plan, true, min_fast_threads);
   if (!err.empty()) return fail(P1HIP_ERR_ARGS, "planner: " + err);
   // Longest-running workgroups first: fast pieces by lo-loop length (10^k),
   // then generic pieces, so short work fills the grid's drain.
@@ -388,44 +404,73 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
         cur += cnt;
       }
     }
+    // Phase 1: every device scans its shard and synchronises its stream.
+    // Phase 2 (the collective) starts only when every device succeeded, so a
+    // failing device can never leave its peers blocked inside ncclAllGather.
     std::vector<int> rcs(nd, 0);
     std::vector<std::string> errs(nd);
-    auto work = [&](size_t i) {
+    auto run_threads = [&](auto&& fn) {
+      if (nd == 1) {
+        fn(0);
+      } else {
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < nd; ++i) th.emplace_back(fn, i);
+        for (auto& t : th) t.join();
+      }
+    };
+    auto first_error = [&]() -> int {
+      for (size_t i = 0; i < nd; ++i)
+        if (rcs[i]) return fail(rcs[i], "device " + std::to_string(R.devs[i].ordinal) + ": " + errs[i]);
+      return P1HIP_OK;
+    };
+    const bool coll = (nd > 1 || R.rccl_one) && R.use_rccl;
+    run_threads([&](size_t i) {
       Dev& d = R.devs[i];
       int r = P1HIP_OK;
-      if (active[i]) {
-        r = run_range(d, msg, msg_len, slo[i], shi[i], R.profiling);
+      if ((int)i == R.fail_device) {
+        r = fail(P1HIP_ERR_HIP, "injected failure (P1HIP_TEST_FAIL_DEVICE)");
+      } else if (active[i]) {
+        r = run_range(d, msg, msg_len, slo[i], shi[i], R.profiling, R.min_fast_threads);
       } else {
         // empty shard: contribute the identity key (all ones)
         if (hipSetDevice(d.ordinal) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipSetDevice");
         if (!r && hipMemsetAsync(d.d_res, 0xFF, sizeof(Key), d.stream) != hipSuccess)
           r = fail(P1HIP_ERR_HIP, "hipMemsetAsync(identity)");
       }
-      if (!r && nd > 1 && R.use_rccl) {
-        ncclResult_t nr = ncclAllGather(d.d_res, d.d_gather, 2, ncclUint64, d.comm, d.stream);
-        if (nr != ncclSuccess) r = fail(P1HIP_ERR_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
-      }
-      if (!r && nd > 1 && !R.use_rccl) {  // host combine (tests)
+      if (!r && !coll && nd > 1) {  // host combine (P1HIP_NO_RCCL, tests)
         if (hipMemcpyAsync(R.devs[0].h_res + i, d.d_res, sizeof(Key), hipMemcpyDeviceToHost, d.stream) != hipSuccess)
           r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(result)");
-      } else if (!r && i == 0) {
-        const Key* src = nd > 1 ? d.d_gather : d.d_res;
-        if (hipMemcpyAsync(d.h_res, src, sizeof(Key) * nd, hipMemcpyDeviceToHost, d.stream) != hipSuccess)
+      } else if (!r && !coll) {
+        if (hipMemcpyAsync(d.h_res, d.d_res, sizeof(Key), hipMemcpyDeviceToHost, d.stream) != hipSuccess)
           r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(result)");
       }
       if (!r && hipStreamSynchronize(d.stream) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipStreamSynchronize");
       rcs[i] = r;
       if (r) errs[i] = g_err;
-    };
-    if (nd == 1) {
-      work(0);
-    } else {
-      std::vector<std::thread> th;
-      for (size_t i = 0; i < nd; ++i) th.emplace_back(work, i);
-      for (auto& t : th) t.join();
+    });
+    if ((rc = first_error()) != P1HIP_OK) return rc;
+    if (coll) {
+      // Phase 2: all-gather the 16-byte partials (2 x u64 per device) over
+      // RCCL; device 0 copies the gathered table to the host.  One group call
+      // per device thread is not needed: each thread enqueues on its own
+      // communicator and the collective completes when all have joined.
+      run_threads([&](size_t i) {
+        Dev& d = R.devs[i];
+        int r = P1HIP_OK;
+        if (hipSetDevice(d.ordinal) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipSetDevice");
+        if (!r) {
+          ncclResult_t nr = ncclAllGather(d.d_res, d.d_gather, 2, ncclUint64, d.comm, d.stream);
+          if (nr != ncclSuccess) r = fail(P1HIP_ERR_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
+        }
+        if (!r && i == 0 &&
+            hipMemcpyAsync(d.h_res, d.d_gather, sizeof(Key) * nd, hipMemcpyDeviceToHost, d.stream) != hipSuccess)
+          r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(gathered)");
+        if (!r && hipStreamSynchronize(d.stream) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipStreamSynchronize");
+        rcs[i] = r;
+        if (r) errs[i] = g_err;
+      });
+      if ((rc = first_error()) != P1HIP_OK) return rc;
     }
-    for (size_t i = 0; i < nd; ++i)
-      if (rcs[i]) return fail(rcs[i], "device " + std::to_string(R.devs[i].ordinal) + ": " + errs[i]);
     Key b = {~0ull, ~0ull};
     for (size_t i = 0; i < nd; ++i) b = key_lt(R.devs[0].h_res[i], b) ? R.devs[0].h_res[i] : b;
     res = finish_key(b);
@@ -465,9 +510,20 @@ int p1hip_reduce_pairs(const uint64_t* hashes, const uint64_t* nonces, size_t n,
   Dev& d = R.devs[0];
   HIPCHK(hipSetDevice(d.ordinal));
   Key res = {~0ull, ~0ull};
+  if (n > (size_t)kMaxLaunchBlocks * kBlock) return fail(P1HIP_ERR_ARGS, "too many pairs");
   if (n) {
     uint64_t *dh = nullptr, *dn = nullptr;
     Key* dp = nullptr;
+    // frees the scratch buffers on every exit path (HIPCHK returns early)
+    struct Scratch {
+      uint64_t **a, **b;
+      Key** c;
+      ~Scratch() {
+        if (*a) (void)hipFree(*a);
+        if (*b) (void)hipFree(*b);
+        if (*c) (void)hipFree(*c);
+      }
+    } scratch{&dh, &dn, &dp};
     const uint32_t blocks = (uint32_t)((n + kBlock - 1) / kBlock);
     HIPCHK(hipMalloc(&dh, n * 8));
     HIPCHK(hipMalloc(&dn, n * 8));
@@ -479,9 +535,6 @@ int p1hip_reduce_pairs(const uint64_t* hashes, const uint64_t* nonces, size_t n,
     HIPCHK(hipMemcpyAsync(d.h_res, d.d_res, sizeof(Key), hipMemcpyDeviceToHost, d.stream));
     HIPCHK(hipStreamSynchronize(d.stream));
     res = d.h_res[0];
-    (void)hipFree(dh);
-    (void)hipFree(dn);
-    (void)hipFree(dp);
   }
   res = finish_key(res);
   *out_hash = res.h;

@@ -234,8 +234,11 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
 
 // Build the launch list for [lower, upper] (inclusive); lower <= upper.
 // `fast_ok` = false routes everything through the generic kernel (tests).
+// `min_fast_threads` is the occupancy floor that lowers k for small decades;
+// tests pass 1 so that k = 3 (and the NV = 2, PRE and TRAIL variants it
+// selects) is exercised on ranges the oracle finishes in seconds.
 inline std::string make_plan(const uint8_t* msg, size_t L, uint64_t lower, uint64_t upper, Plan& plan,
-                             bool fast_ok = true) {
+                             bool fast_ok = true, uint64_t min_fast_threads = kMinFastThreads) {
   Prefix P;
   make_prefix(msg, L, P);
   plan = Plan();
@@ -248,7 +251,7 @@ inline std::string make_plan(const uint8_t* msg, size_t L, uint64_t lower, uint6
     Layout Y = make_layout(P.r, d);
     // smaller k keeps the lo digits inside the same block (they are a suffix
     // of make_layout's k digits), so any k <= Y.k is a valid layout
-    while (Y.k > 1 && (e - s) / pow10u(Y.k) + 1 < kMinFastThreads) --Y.k;
+    while (Y.k > 1 && (e - s) / pow10u(Y.k) + 1 < min_fast_threads) --Y.k;
     if (!fast_ok || d <= Y.k) {
       add_generic(P, Y, s, e, plan);
       continue;

@@ -8,8 +8,9 @@
 //   p1miner hash <msg> <nonce>           prints bitcoin.Hash(msg, nonce)
 //   p1miner serve [--device N] [--chunk C]
 //                                        one JSON Message per stdin line; every
-//                                        Request is answered with one JSON
-//                                        Result line (Join/Result lines ignored)
+//                                        line is answered with one JSON Result
+//                                        line (miner.go:49-67 scans whatever it
+//                                        decoded; a bad line scans [0, 0] of "")
 //   p1miner json                         re-marshals stdin JSON lines (no GPU;
 //                                        wire-format tests)
 //   p1miner lsp-json                     re-marshals stdin lsp.Message JSON lines
@@ -125,9 +126,12 @@ int main(int argc, char** argv) {
       if (rc != P1HIP_OK) { fprintf(stderr, "p1hip init: %s\n", p1hip_last_error()); return 1; }
       std::string line;
       while (std::getline(std::cin, line)) {
+        // miner.go:54-55 decodes into a zero Message and ignores the error, then
+        // scans [Lower, Upper] whatever the Type: an undecodable line is the
+        // one-nonce request ("", [0, 0]) and is answered like any other, so a
+        // server never waits on a miner that stays silent.
         bitcoin::Message req;
-        if (!bitcoin::Unmarshal(line, &req)) continue;  // miner.go:55 ignores decode errors
-        if (req.Type != bitcoin::Request) continue;
+        if (!bitcoin::Unmarshal(line, &req)) req = bitcoin::Message();
         bitcoin::Message res = miner::HandleRequest(req, chunk);
         printf("%s\n", bitcoin::Marshal(res).c_str());
         fflush(stdout);

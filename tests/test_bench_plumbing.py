@@ -1,0 +1,74 @@
+"""CPU tests of bench.py's launch plumbing: how --gpus, WORLD_SIZE and the
+visible device count decide the mode, the job and the default workload
+(VERDICT r01 "make the N>1 bench driver-proof")."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_single_gpu_defaults_to_c2():
+    r = bench.resolve_run(1, None, {}, visible=1)
+    assert r["mode"] == "single" and r["n"] == 1 and r["config"] == "c2"
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_library_path_without_torchrun(n):
+    # `python bench.py --gpus N` (no WORLD_SIZE): one process, N devices in the library
+    r = bench.resolve_run(n, None, {}, visible=8)
+    assert r["mode"] == "library" and r["n"] == n and r["world"] == 1
+    assert r["config"] == "c4"  # the fixed [0, 2^38) job at N > 1
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_torchrun_path(n):
+    env = {"WORLD_SIZE": str(n), "RANK": "1", "LOCAL_RANK": "1"}
+    r = bench.resolve_run(n, None, env, visible=8)
+    assert r["mode"] == "torchrun" and r["n"] == n and r["rank"] == 1 and r["config"] == "c4"
+
+
+def test_more_gpus_than_visible_is_an_error():
+    with pytest.raises(bench.UsageError):
+        bench.resolve_run(8, None, {}, visible=1)
+    with pytest.raises(bench.UsageError):
+        bench.resolve_run(0, None, {}, visible=1)
+
+
+def test_torchrun_world_mismatch_is_an_error():
+    with pytest.raises(bench.UsageError):
+        bench.resolve_run(4, None, {"WORLD_SIZE": "2"}, visible=8)
+
+
+def test_explicit_config_wins():
+    assert bench.resolve_run(1, "c4", {}, visible=1)["config"] == "c4"
+    assert bench.resolve_run(8, "c2", {}, visible=8)["config"] == "c2"
+
+
+def test_job_sizes():
+    assert bench.job_total(bench.CONFIGS["c4"], 1) == 1 << 38
+    assert bench.job_total(bench.CONFIGS["c4"], 8) == 1 << 38  # strong scaling: fixed job
+    assert bench.job_total(bench.CONFIGS["c2"], 8) == 8 << 32  # weak scaling
+    assert bench.known_answer(bench.CONFIGS["c4"], 8) == bench.known_answer(bench.CONFIGS["c4"], 1)
+    assert bench.known_answer(bench.CONFIGS["c2"], 1) == (5256245051, 1626825724)
+
+
+def test_cli_refuses_more_gpus_than_visible():
+    # no GPU in this container: --gpus 2 must exit non-zero, never run on fewer
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert p.returncode != 0
+    assert "visible" in p.stderr
+
+
+def test_host_cores_reports_model():
+    n, aff, quota, model = bench.host_cores()
+    assert 1 <= n <= aff and model

@@ -1,0 +1,119 @@
+"""GPU tests of the library paths the r01 suite did not reach:
+
+* k = 3 fast path on every layout: the planner's occupancy floor
+  (P1HIP_MIN_FAST_THREADS, test-only) set to 1 keeps k = 3 -- and with it the
+  NV = 2, PRE and TRAIL variants and the tens/hundreds carry deltas -- on
+  ranges the oracle finishes in seconds;
+* the RCCL combine (ncclCommInitAll + ncclAllGather) on a one-device
+  communicator (P1HIP_FORCE_RCCL=1), the only RCCL shape a 1-GPU box can run;
+* the multi-device error path: a failure injected on one device returns an
+  error instead of blocking its peers in the collective, and the library is
+  usable afterwards;
+* configs[4] at full size: p1server splits [0, 2^36) over 8 p1miner
+  processes sharing GPU 0.
+
+Every env knob is read at init, so each test re-initialises the library.
+Reference: miner.go:56-63 (scan), server.go:119-140 (dispatch)."""
+import os
+import random
+import subprocess
+import time
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+U64_MAX = (1 << 64) - 1
+
+
+@pytest.fixture
+def reinit(gpu, monkeypatch):
+    """Set env knobs, re-initialise on the given devices; restore after."""
+    def go(ordinals=(0,), **env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, str(v))
+        gpu.shutdown()
+        gpu.init_devices(list(ordinals))
+        return gpu
+
+    yield go
+    for k in ("P1HIP_MIN_FAST_THREADS", "P1HIP_FORCE_RCCL", "P1HIP_TEST_FAIL_DEVICE", "P1HIP_NO_RCCL"):
+        monkeypatch.delenv(k, raising=False)
+    gpu.shutdown()
+    gpu.init_devices([0])
+
+
+def test_k3_every_layout_vs_oracle(reinit, oracle_mod):
+    g = reinit(P1HIP_MIN_FAST_THREADS=1)
+    rnd = random.Random(31)
+    g.reset_stats()
+    for L in range(0, 130):
+        m = bytes(rnd.randrange(32, 127) for _ in range(L))
+        for d in (5, 9, 10, 11, 12, 20):
+            b = 10 ** (d - 1)
+            lo = b + rnd.randrange(0, 10**4) if d < 20 else b
+            hi = min(lo + rnd.randrange(3000, 9000), U64_MAX)
+            assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
+    s = g.get_stats()
+    # most nonces went through the fast (10^k loop) kernels, not the generic one
+    assert s["fast_nonces"] > 3 * s["generic_nonces"]
+
+
+def test_k3_straddles_and_edges(reinit, oracle_mod):
+    g = reinit(P1HIP_MIN_FAST_THREADS=1)
+    rnd = random.Random(32)
+    for L in (0, 8, 45, 53, 54, 55, 56, 62, 63, 64, 119, 120, 127):
+        m = bytes(rnd.randrange(32, 127) for _ in range(L))
+        for d in range(4, 21):
+            b = 10 ** (d - 1)
+            lo, hi = max(0, b - 2345), min(b + 6789, U64_MAX)
+            assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (L, d)
+    for m in (b"msg", b"y" * 61):
+        assert g.scan(m, U64_MAX - 7000, U64_MAX) == oracle_mod.scan(m, U64_MAX - 7000, U64_MAX, threads=8)
+
+
+def test_rccl_allgather_one_device(reinit, oracle_mod):
+    g = reinit(P1HIP_FORCE_RCCL=1)
+    for m, lo, hi in [(b"bradfitz", 0, 9999), (b"msg", 0, 2), (b"msg", 7, 3), (b"x" * 70, 10**9 - 3000, 10**9 + 3000)]:
+        assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8)
+    assert g.scan("bradfitz", 0, (1 << 32) - 1) == (5256245051, 1626825724)
+
+
+def test_failure_on_one_device_does_not_hang(reinit, oracle_mod):
+    g = reinit((0, 0), P1HIP_NO_RCCL=1, P1HIP_TEST_FAIL_DEVICE=1)
+    t0 = time.time()
+    with pytest.raises(g.P1HipError) as e:
+        g.scan("bradfitz", 0, 99999)
+    assert e.value.rc == -2 and "injected" in str(e.value)
+    assert time.time() - t0 < 30
+    # the collective path: the failing device is the only member; the all-gather is skipped
+    g = reinit((0,), P1HIP_NO_RCCL=0, P1HIP_FORCE_RCCL=1, P1HIP_TEST_FAIL_DEVICE=0)
+    with pytest.raises(g.P1HipError):
+        g.scan("bradfitz", 0, 99999)
+    # the library is usable afterwards
+    g = reinit((0,), P1HIP_TEST_FAIL_DEVICE=-1, P1HIP_FORCE_RCCL=0)
+    assert g.scan("bradfitz", 0, 9999) == (1419516646206828, 9898)
+
+
+def test_config5_full_size_split_over_8_miner_processes(gpu, oracle_mod):
+    """configs[4]'s job -- [0, 2^36) split by the server into 2^32-nonce
+    chunks over 8 GPU miner processes (here all on GPU 0) -- checked by
+    size-independent properties: the reported nonce re-hashes to the
+    reported hash on the oracle, and the result equals the min of two
+    independently scanned halves."""
+    server = os.path.join(ROOT, "p1_amd", "p1server")
+    hi = (1 << 36) - 1
+    t0 = time.time()
+    r = subprocess.run([server, "--miners", "8", "--devices", "0", "--chunk", str(1 << 32), "scan", "bradfitz",
+                        "0", str(hi)], capture_output=True, text=True, timeout=300)
+    wall = time.time() - t0
+    assert r.returncode == 0, r.stderr
+    word, h, n = r.stdout.split()
+    h, n = int(h), int(n)
+    assert word == "Result"
+    assert oracle_mod.hash("bradfitz", n) == h
+    a = gpu.scan("bradfitz", 0, (1 << 35) - 1)
+    b = gpu.scan("bradfitz", 1 << 35, hi)
+    assert min(a, b) == (h, n)
+    print(f"configs[4] over stdio: 2^36 nonces, 8 miners on one GPU, {wall:.2f} s wall")

@@ -15,8 +15,10 @@ U64_MAX = (1 << 64) - 1
 EMU = os.path.join(ROOT, "tools", "p1emu")
 
 
-def emu(msg, lo, hi, generic=False):
+def emu(msg, lo, hi, generic=False, minthreads=None):
     args = [EMU, msg.hex() if msg else "-", str(lo), str(hi)] + (["generic"] if generic else [])
+    if minthreads is not None:
+        args.append(f"minthreads={minthreads}")
     out = subprocess.run(args, capture_output=True, text=True, check=True).stdout.split()
     return (int(out[0]), int(out[1])), int(out[2]), int(out[3])
 
@@ -58,6 +60,22 @@ def test_emu_every_layout(oracle_mod):
             lo = b + rnd.randrange(0, 10**4)
             hi = min(lo + 1999, U64_MAX)
             got, nf, _ = emu(m, lo, hi)
+            assert nf >= 1
+            assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
+
+
+def test_emu_every_layout_k3(oracle_mod):
+    """Planner occupancy floor at 1 thread: k = 3 on small ranges, so every
+    (FV, NV, TRAIL) variant, PRE/TRAIL at k = 3 and the tens/hundreds carry
+    deltas (dt/dhd) are replayed against the oracle."""
+    rnd = random.Random(8)
+    for L in range(0, 128):
+        m = bytes(rnd.randrange(32, 127) for _ in range(L))
+        for d in (5, 9, 10, 11, 12, 20):
+            b = 10 ** (d - 1)
+            lo = b + rnd.randrange(0, 10**4) if d < 20 else b
+            hi = min(lo + 4999, U64_MAX)
+            got, nf, _ = emu(m, lo, hi, minthreads=1)
             assert nf >= 1
             assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
 

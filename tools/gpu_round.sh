@@ -19,10 +19,13 @@ step() {  # step <name> <timeout> <cmd...>
 }
 [ "${SKIP_PEAK:-0}" = 1 ] || step valu_peak 300 "$ROOT/tools/valu_peak" > "$OUT/${TAG}_valu_peak.jsonl"
 [ "${RUN_MIX:-0}" != 1 ] || step valu_mix 300 "$ROOT/tools/valu_mix" > "$OUT/${TAG}_valu_mix.jsonl"
-[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest "$ROOT/tests" -m gpu -x -q -p no:cacheprovider > "$OUT/${TAG}_pytest_gpu.log" 2>&1
+[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -u -m pytest "$ROOT/tests" -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/${TAG}_pytest_gpu.log" 2>&1
 [ "${SKIP_SMOKE:-0}" = 1 ] || step smoke 300 python -c "import sys; sys.path.insert(0, '$ROOT'); import __graft_entry__ as g; g.smoke()" > "$OUT/${TAG}_smoke.log" 2>&1
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 600 python "$ROOT/bench.py" ${BENCH_ARGS:-} > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
 [ -z "${EXTRA_BENCH:-}" ] || step bench_extra 600 python "$ROOT/bench.py" $EXTRA_BENCH > "$OUT/${TAG}_bench_extra.json" 2> "$OUT/${TAG}_bench_extra.err"
+for cfg in ${BENCH_CONFIGS:-}; do
+  step bench_$cfg 600 python "$ROOT/bench.py" --config $cfg --steps ${CFG_STEPS:-3} --warmup 1 --no-cpu > "$OUT/${TAG}_bench_$cfg.json" 2> "$OUT/${TAG}_bench_$cfg.err"
+done
 [ "${RUN_SWEEP:-0}" != 1 ] || step sweep 900 python "$ROOT/tools/sweep.py" > "$OUT/${TAG}_sweep.jsonl" 2> "$OUT/${TAG}_sweep.err"
 [ "${RUN_SERVER:-0}" != 1 ] || step bench_server 900 python "$ROOT/tools/bench_server.py" > "$OUT/${TAG}_bench_server.json" 2> "$OUT/${TAG}_bench_server.err"
 if [ "${RUN_TORCHRUN:-0}" = 1 ]; then
@@ -34,14 +37,22 @@ for lib in ${VARIANTS:-}; do
   P1HIP_LIB="$ROOT/$lib" step "bench_$n" 600 python "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu > "$OUT/${TAG}_bench_$n.json" 2> "$OUT/${TAG}_bench_$n.err"
 done
 cd /tmp && export TMPDIR=/tmp
-if [ "${SKIP_PROF:-0}" != 1 ]; then
-  step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-small-request
-fi
-if [ "${SKIP_PMC:-0}" != 1 ]; then
-  i=0
-  for set in "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE"; do
-    i=$((i+1))
-    step pmc$i 600 rocprofv3 --pmc $set --kernel-include-regex '^k_scan' -d "$OUT/${TAG}_pmc$i" -o pmc --output-format csv -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu --no-small-request
-  done
-fi
+# kernel-trace stats and PMC passes per config (every k_scan launch of the
+# profiled command is a workload launch: --no-small-request)
+for cfg in ${PROF_CONFIGS:-c2}; do
+  pargs="--steps 1 --warmup 0 --no-cpu --no-small-request --config $cfg"
+  if [ "${SKIP_PROF:-0}" != 1 ]; then
+    step rocprof_stats_$cfg 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_${cfg}_prof" -o run --output-format csv -- python3 "$ROOT/bench.py" $pargs
+  fi
+  if [ "${SKIP_PMC:-0}" != 1 ]; then
+    i=0
+    for set in "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_INSTS_VALU_INT32 SQ_INSTS_SALU" \
+               "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE" \
+               "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_IFETCH" \
+               "FETCH_SIZE" "WRITE_SIZE"; do
+      i=$((i+1))
+      step pmc_${cfg}_$i 300 rocprofv3 --pmc $set --kernel-include-regex '^k_scan' -d "$OUT/${TAG}_${cfg}_pmc$i" -o pmc --output-format csv -- python3 "$ROOT/bench.py" $pargs
+    done
+  fi
+done
 echo "== done"

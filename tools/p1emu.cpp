@@ -7,7 +7,9 @@
 // CPU-only test suite.  It is never part of libp1hip.so and never used to
 // produce a product result.
 //
-// usage: p1emu <msg-hex> <lower> <upper> [generic]
+// usage: p1emu <msg-hex> <lower> <upper> [generic | minthreads=N]
+//   minthreads=N sets the planner's occupancy floor (1 keeps k = 3 on small
+//   ranges, so every k = 3 variant is replayed)
 //   prints "<hash> <nonce> <fast_launches> <generic_launches>"
 #include <inttypes.h>
 #include <stdio.h>
@@ -53,18 +55,20 @@ static std::vector<uint8_t> unhex(const char* s) {
 
 int main(int argc, char** argv) {
   if (argc < 4) {
-    fprintf(stderr, "usage: %s <msg-hex|-> <lower> <upper> [generic]\n", argv[0]);
+    fprintf(stderr, "usage: %s <msg-hex|-> <lower> <upper> [generic|minthreads=N]\n", argv[0]);
     return 2;
   }
   std::vector<uint8_t> msg = strcmp(argv[1], "-") == 0 ? std::vector<uint8_t>() : unhex(argv[1]);
   const uint64_t lower = strtoull(argv[2], nullptr, 10);
   const uint64_t upper = strtoull(argv[3], nullptr, 10);
   const bool generic_only = argc > 4 && strcmp(argv[4], "generic") == 0;
+  uint64_t min_threads = kMinFastThreads;
+  if (argc > 4 && strncmp(argv[4], "minthreads=", 11) == 0) min_threads = strtoull(argv[4] + 11, nullptr, 10);
   Key best = {~0ull, ~0ull};
   int nf = 0, ng = 0;
   if (lower <= upper) {
     Plan plan;
-    std::string err = make_plan(msg.data(), msg.size(), lower, upper, plan, !generic_only);
+    std::string err = make_plan(msg.data(), msg.size(), lower, upper, plan, !generic_only, min_threads);
     if (!err.empty()) {
       fprintf(stderr, "plan error: %s\n", err.c_str());
       return 1;

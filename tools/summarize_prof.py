@@ -1,12 +1,16 @@
 """Copy one GPU session's rocprofv3 outputs from gpurun_out/ into profiles/
 and write a JSON summary of the scan kernel's counters.
 
-usage: python tools/summarize_prof.py <TAG> [nonces_per_launch]
+usage: python tools/summarize_prof.py <TAG> [nonces_per_launch] [--config cN --nonces-total N]
   reads  gpurun_out/<TAG>_prof/run_kernel_stats.csv  (--kernel-trace --stats)
          gpurun_out/<TAG>_pmc*/pmc_counter_collection.csv (--pmc passes)
          gpurun_out/<TAG>_bench*.json, <TAG>_valu_*.jsonl
   writes profiles/<TAG>_kernel_stats.csv, profiles/<TAG>_pmc_summary.json,
          profiles/<TAG>_bench*.json, profiles/<TAG>_valu_*.jsonl
+  With --nonces-total (the nonces the profiled command scanned, every k_scan
+  launch of it a workload launch: bench.py --no-small-request), per-nonce
+  figures come from counters summed over ALL its launches -- needed when a
+  step is several launches (configs[3]: 2 per 2^38 scan).
 """
 import csv
 import glob
@@ -34,9 +38,25 @@ def workload_stats(trace, out):
         f.write(f'"k_scan",{len(d)},{sum(d)},{mean:.1f},{min(d)},{max(d)},{sd:.1f},{g},"{os.path.basename(trace)}"\n')
 
 
+# Measured issue cost (SIMD cycles per wave instruction at 4 waves/SIMD,
+# 8-byte encodings at 4 mod 8: DESIGN.md 4 "What bounds it") of the two
+# integer-VALU classes; used to price an executed mix.
+ISSUE_COST_HALF = 4.37   # v_alignbit_b32, v_add3_u32 and the other 3-input VOP3 ops
+ISSUE_COST_FULL = 2.66   # v_bitop3_b32, v_add_u32_e64, v_lshrrev_b32_e64, ...
+
+
 def main():
-    tag = sys.argv[1]
-    nonces = float(sys.argv[2]) if len(sys.argv) > 2 else 2.0**32
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("nonces_per_launch", nargs="?", type=float, default=2.0**32)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--nonces-total", type=float, default=None)
+    ap.add_argument("--half-rate-share", type=float, default=None,
+                    help="share of class-A (half-rate) instructions in the executed loop mix")
+    a = ap.parse_args()
+    tag, nonces = a.tag, a.nonces_per_launch
     src = os.path.join(ROOT, "gpurun_out")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -48,7 +68,7 @@ def main():
         workload_stats(kt, os.path.join(dst, f"{tag}_kernel_stats_workload.csv"))
     for f in glob.glob(os.path.join(src, f"{tag}_bench*.json")) + glob.glob(os.path.join(src, f"{tag}_valu_*.jsonl")):
         shutil.copy(f, os.path.join(dst, os.path.basename(f)))
-    counters, durs = {}, []
+    counters, durs, sums = {}, [], {}
     for f in sorted(glob.glob(os.path.join(src, f"{tag}_pmc*", "*counter_collection.csv"))):
         rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("k_scan")]
         if not rows:
@@ -57,6 +77,7 @@ def main():
         # small configs[0]-sized requests whose launches are not the roofline kernel
         gmax = max(int(r["Grid_Size"]) for r in rows)
         for r in rows:
+            sums[r["Counter_Name"]] = sums.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
             if int(r["Grid_Size"]) != gmax:
                 continue
             counters.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
@@ -66,15 +87,41 @@ def main():
         return
     avg = {k: sum(v) / len(v) for k, v in counters.items()}
     dur = sum(durs) / len(durs)
-    out = {"tag": tag, "kernel": "k_scan", "avg_duration_s": dur, "counters_per_launch": avg}
+    out = {"tag": tag, "config": a.config, "kernel": "k_scan", "avg_duration_s": dur,
+           "counters_per_launch": avg}
+    if a.nonces_total:
+        out["nonces_total"] = a.nonces_total
+        out["counters_total"] = sums
     if "GRBM_GUI_ACTIVE" in avg:
         out["effective_clock_GHz"] = avg["GRBM_GUI_ACTIVE"] / 8 / dur / 1e9  # summed over 8 XCDs
     if "SQ_INSTS_VALU" in avg:
-        out["valu_wave_instr_per_nonce"] = avg["SQ_INSTS_VALU"] * 64 / nonces
+        if a.nonces_total:
+            out["valu_wave_instr_per_nonce"] = sums["SQ_INSTS_VALU"] * 64 / a.nonces_total
+        else:
+            out["valu_wave_instr_per_nonce"] = avg["SQ_INSTS_VALU"] * 64 / nonces
         if "effective_clock_GHz" in out:
             simd_cycles = dur * out["effective_clock_GHz"] * 1e9 * 1024
             out["simd_cycles_per_valu_wave_instr"] = simd_cycles / avg["SQ_INSTS_VALU"]
             out["valu_issue_frac_of_2cyc_peak"] = 2.0 / out["simd_cycles_per_valu_wave_instr"]
+            if a.half_rate_share is not None:
+                # executed mix priced at the measured class issue costs / SIMD cycles spent
+                price = a.half_rate_share * ISSUE_COST_HALF + (1 - a.half_rate_share) * ISSUE_COST_FULL
+                out["half_rate_share"] = a.half_rate_share
+                out["issue_frac"] = price / out["simd_cycles_per_valu_wave_instr"]
+    if "SQ_ACTIVE_INST_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
+        # VALUBusy's own expression (rocprofv3 --list-avail): quad-cycles of
+        # VALU work per CU over GPU cycles (GRBM_GUI_ACTIVE is summed over 8 XCDs)
+        gpu_cycles = avg["GRBM_GUI_ACTIVE"] / 8
+        out["valu_busy_frac"] = avg["SQ_ACTIVE_INST_VALU"] * 4 / 256 / gpu_cycles / 4
+        out["valu_busy_note"] = ("SQ_ACTIVE_INST_VALU x 4 cycles / (256 CUs x 4 SIMDs x GPU cycles); "
+                                 "on gfx950 this counter equals SQ_INSTS_VALU (one count per wave "
+                                 "instruction), so it measures issue slots, not busy cycles")
+    if "SQ_THREAD_CYCLES_VALU" in avg and "SQ_INSTS_VALU" in avg:
+        out["thread_cycles_valu_per_wave_instr"] = avg["SQ_THREAD_CYCLES_VALU"] / avg["SQ_INSTS_VALU"]
+    if "SQ_ACTIVE_INST_VALU2" in avg and "SQ_INSTS_VALU" in avg:
+        out["dual_valu_issue_quads_per_wave_instr"] = avg["SQ_ACTIVE_INST_VALU2"] / avg["SQ_INSTS_VALU"]
+    if "SQ_BUSY_CU_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg:
+        out["cu_busy_frac"] = avg["SQ_BUSY_CU_CYCLES"] * 4 / 256 / (avg["GRBM_GUI_ACTIVE"] / 8)
     if "FETCH_SIZE" in avg or "WRITE_SIZE" in avg:
         # FETCH_SIZE/WRITE_SIZE are KB; gfx950 FETCH_SIZE under-counts wide streaming reads 2x
         # (MI355X_MICROARCH.md HBM section) -- this kernel has no such reads (kernel args,
