@@ -14,7 +14,8 @@ DEVFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) --cuda-device-only -Wall $(DEV
 ISAPOST ?= --align-loops=3 --loop-offset=4 --loop-parity
 BUILD := build
 
-all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server
+all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios \
+     tools/lsp_fake_miner
 
 $(BUILD)/p1hip_kernels.s: $(CSRC)/p1hip_kernels.hip $(HDRS)
 	mkdir -p $(BUILD)
@@ -39,15 +40,31 @@ $(BUILD)/p1hip_host.o: $(CSRC)/p1hip.hip $(HDRS)
 p1_amd/libp1hip.so: $(BUILD)/p1hip_host.o $(BUILD)/p1hip_kernels_blob.o
 	$(HIPCC) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
-# C++ host mirror of the reference's bitcoin package + miner loop (stdio)
-HOSTSRC := p1_amd/host/bitcoin.cpp p1_amd/host/lsp_message.cpp
-HOSTHDR := p1_amd/host/bitcoin.hpp p1_amd/host/lsp_message.hpp p1_amd/host/gojson.hpp include/p1hip.h
+# C++ host mirror of the reference's bitcoin package, LSP transport and the
+# miner / server / client programs
+HOSTSRC := p1_amd/host/bitcoin.cpp p1_amd/host/lsp_message.cpp p1_amd/host/lsp.cpp p1_amd/host/lspnet.cpp
+HOSTHDR := p1_amd/host/bitcoin.hpp p1_amd/host/lsp_message.hpp p1_amd/host/gojson.hpp p1_amd/host/lsp.hpp \
+           p1_amd/host/lspnet.hpp p1_amd/host/scheduler.hpp include/p1hip.h
+HOSTFLAGS := -O2 -std=c++17 -Wall -Wextra -pthread
 
-p1_amd/p1miner: p1_amd/host/p1miner.cpp $(HOSTSRC) $(HOSTHDR) p1_amd/libp1hip.so
-	g++ -O2 -std=c++17 -Wall -Wextra -o $@ p1_amd/host/p1miner.cpp $(HOSTSRC) -Lp1_amd -lp1hip -Wl,-rpath,'$$ORIGIN'
+p1_amd/p1miner: p1_amd/host/p1miner.cpp p1_amd/host/miner_gpu.cpp $(HOSTSRC) $(HOSTHDR) p1_amd/libp1hip.so
+	g++ $(HOSTFLAGS) -o $@ p1_amd/host/p1miner.cpp p1_amd/host/miner_gpu.cpp $(HOSTSRC) -Lp1_amd -lp1hip -Wl,-rpath,'$$ORIGIN'
 
-p1_amd/p1server: p1_amd/host/p1server.cpp $(HOSTSRC) $(HOSTHDR) p1_amd/libp1hip.so
-	g++ -O2 -std=c++17 -Wall -Wextra -o $@ p1_amd/host/p1server.cpp $(HOSTSRC) -Lp1_amd -lp1hip -Wl,-rpath,'$$ORIGIN'
+# the server schedules; its pipe-transport miners are p1miner processes
+p1_amd/p1server: p1_amd/host/p1server.cpp $(HOSTSRC) $(HOSTHDR)
+	g++ $(HOSTFLAGS) -o $@ p1_amd/host/p1server.cpp $(HOSTSRC)
+
+# the client never touches the GPU (client.go): no libp1hip link
+p1_amd/p1client: p1_amd/host/p1client.cpp $(HOSTSRC) $(HOSTHDR)
+	g++ $(HOSTFLAGS) -o $@ p1_amd/host/p1client.cpp $(HOSTSRC)
+
+# test driver: the reference's LSP test scenarios (tests/test_lsp.py)
+tools/lsp_scenarios: tests/lsp/lsp_scenarios.cpp p1_amd/host/lsp.cpp p1_amd/host/lspnet.cpp p1_amd/host/lsp_message.cpp $(HOSTHDR)
+	g++ $(HOSTFLAGS) -o $@ tests/lsp/lsp_scenarios.cpp p1_amd/host/lsp.cpp p1_amd/host/lspnet.cpp p1_amd/host/lsp_message.cpp
+
+# test double: an LSP miner answering with the CPU oracle (tests/test_lsp_bitcoin.py)
+tools/lsp_fake_miner: tests/lsp/lsp_fake_miner.cpp p1_amd/host/bitcoin.cpp $(HOSTSRC) $(HOSTHDR) oracle
+	g++ $(HOSTFLAGS) -o $@ tests/lsp/lsp_fake_miner.cpp $(HOSTSRC) -Loracle -lp1oracle -Wl,-rpath,'$$ORIGIN/../oracle'
 
 # host-only replay of the kernels' per-thread code (layout tests; not product)
 tools/p1emu: tools/p1emu.cpp $(HDRS)
@@ -69,7 +86,7 @@ isa: $(BUILD)/p1hip_kernels.post.s
 	$(HIPCC) $(DEVFLAGS) -c -o /dev/null $(CSRC)/p1hip_kernels.hip -Rpass-analysis=kernel-resource-usage 2> $(BUILD)/resource.txt || true
 
 clean:
-	rm -f p1_amd/libp1hip.so tools/p1emu p1_amd/p1miner p1_amd/p1server
+	rm -f p1_amd/libp1hip.so tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios tools/lsp_fake_miner
 	rm -rf $(BUILD)/p1hip_kernels* $(BUILD)/p1hip_host.o
 	$(MAKE) -C oracle clean
 .PHONY: all oracle clean isa variant

@@ -108,7 +108,13 @@ extern "C" __global__ __launch_bounds__(kBlock, P1_FAST_WAVES) void k_scan(const
   case variant_id(FV, NV, TR):                      \
     k = fast_thread<FV, NV, TR>(S.fa, local);       \
     break;
+// P1_VARIANTS_INC: a subset of the variant list (tools/variant_report.py
+// builds one variant per code object to read its registers and loop mix)
+#ifdef P1_VARIANTS_INC
+#include P1_VARIANTS_INC
+#else
 #include "fast_variants.inc"
+#endif
 #undef P1_CASE
     default:
       k = generic_thread(S.ga, local);

@@ -1,5 +1,6 @@
-// bitcoin.cpp -- see bitcoin.hpp.  Host code only: every hash is computed
-// by libp1hip.so on the GPU.
+// bitcoin.cpp -- see bitcoin.hpp: the Message type and its encoding/json
+// wire form (no GPU here; bitcoin::Hash and the miner loop, which call
+// libp1hip.so, are in miner_gpu.cpp).
 #include "bitcoin.hpp"
 
 #include <inttypes.h>
@@ -8,7 +9,6 @@
 #include <cctype>
 #include <cstring>
 
-#include "../../include/p1hip.h"
 #include "gojson.hpp"
 
 namespace bitcoin {
@@ -49,16 +49,6 @@ std::string Message::String() const {
       return "[Join]";
   }
   return "";
-}
-
-static void check(int rc) {
-  if (rc != P1HIP_OK) throw HipError(rc, std::string("p1hip: ") + p1hip_last_error());
-}
-
-uint64_t Hash(const std::string& msg, uint64_t nonce) {
-  uint64_t h = 0;
-  check(p1hip_hash(reinterpret_cast<const uint8_t*>(msg.data()), msg.size(), nonce, &h));
-  return h;
 }
 
 std::string Marshal(const Message& m) {
@@ -116,36 +106,3 @@ bool Unmarshal(const std::string& json, Message* out) {
 }
 
 }  // namespace bitcoin
-
-namespace miner {
-
-void ScanChunked(const std::string& msg, uint64_t lower, uint64_t upper, uint64_t chunk, uint64_t* hash,
-                 uint64_t* nonce) {
-  uint64_t best = UINT64_MAX, bi = 0;
-  bool found = false;
-  if (chunk == 0) chunk = kDefaultChunk;
-  if (lower <= upper) {
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(msg.data());
-    for (uint64_t lo = lower;;) {
-      const uint64_t hi = (upper - lo >= chunk) ? lo + (chunk - 1) : upper;
-      uint64_t h = 0, n = 0;
-      int rc = p1hip_scan(p, msg.size(), lo, hi, &h, &n);
-      if (rc != P1HIP_OK) throw bitcoin::HipError(rc, std::string("p1hip_scan: ") + p1hip_last_error());
-      // chunks are visited in increasing nonce order: strict '<' keeps the
-      // first minimum (miner.go:59); an all-MaxUint64 chunk reads (Max, 0)
-      if (h < best) { best = h; bi = n; found = true; }
-      if (hi == upper) break;
-      lo = hi + 1;
-    }
-  }
-  *hash = best;
-  *nonce = found ? bi : 0;
-}
-
-bitcoin::Message HandleRequest(const bitcoin::Message& req, uint64_t chunk) {
-  uint64_t h = 0, n = 0;
-  ScanChunked(req.Data, req.Lower, req.Upper, chunk, &h, &n);
-  return bitcoin::NewResult(h, n);
-}
-
-}  // namespace miner

@@ -1,7 +1,15 @@
-// p1miner -- the miner's Request -> Result loop (miner.go:49-67) over stdio,
-// GPU-backed through libp1hip.so.  The LSP transport (SRC/lsp) is out of
-// scope; requests/results are the same encoding/json bitcoin.Message bytes
-// the reference puts in LSP payloads (miner.go:55,66).
+// p1miner -- the miner's Request -> Result loop (miner.go:49-67), GPU-backed
+// through libp1hip.so, over LSP (the reference's transport) or stdio.
+// Requests/results are encoding/json bitcoin.Message bytes (miner.go:55,66).
+//
+//   p1miner lsp <host:port> [--device N] [--chunk C] [--epoch-limit K]
+//           [--epoch-millis M] [--window W]
+//                                        miner.go:13-73: connect, send Join,
+//                                        then Read -> scan -> Write until the
+//                                        connection is lost.  The scan runs on
+//                                        this thread while the LSP event loop
+//                                        keeps heartbeating, so a long GPU job
+//                                        never trips the epoch limit.
 //
 //   p1miner scan <msg> <lower> <upper>   prints "Result <hash> <nonce>"
 //                                        (the client's output, client.go:59-61)
@@ -27,16 +35,20 @@
 #include <string.h>
 
 #include <iostream>
+#include <memory>
 #include <string>
 
 #include "../../include/p1hip.h"
 #include "bitcoin.hpp"
+#include "lsp.hpp"
 #include "lsp_message.hpp"
+#include "lspnet.hpp"
 
 static int usage() {
   fprintf(stderr,
           "usage: p1miner scan <msg> <lower> <upper> | hash <msg> <nonce> | "
-          "serve [--device N] [--chunk C] | json | lsp-json | lsp-wrap <connID> <seq> | lsp-unwrap\n");
+          "serve [--device N] [--chunk C] | lsp <host:port> [--device N] [--chunk C] [--epoch-limit K] "
+          "[--epoch-millis M] [--window W] | json | lsp-json | lsp-wrap <connID> <seq> | lsp-unwrap\n");
   return 2;
 }
 
@@ -50,10 +62,53 @@ static bool parse_u64(const char* s, uint64_t* v) {
   return true;
 }
 
+// miner.go:13-31 (joinWithServer) + miner.go:33-73 (main loop)
+static int run_lsp(int argc, char** argv) {
+  const std::string hostport = argv[2];
+  int dev = -1;
+  uint64_t chunk = miner::kDefaultChunk;
+  lsp::Params prm = lsp::NewParams();
+  for (int i = 3; i < argc; ++i) {
+    if (!strcmp(argv[i], "--device") && i + 1 < argc) dev = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--chunk") && i + 1 < argc) { if (!parse_u64(argv[++i], &chunk)) return usage(); }
+    else if (!strcmp(argv[i], "--epoch-limit") && i + 1 < argc) prm.EpochLimit = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--epoch-millis") && i + 1 < argc) prm.EpochMillis = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--window") && i + 1 < argc) prm.WindowSize = atoi(argv[++i]);
+    else return usage();
+  }
+  // open the GPU before joining, so the first request does not pay for it
+  int rc = dev >= 0 ? p1hip_init_devices(&dev, 1) : p1hip_init(0, nullptr);
+  if (rc != P1HIP_OK) { fprintf(stderr, "p1hip init: %s\n", p1hip_last_error()); return 1; }
+  std::string err;
+  std::unique_ptr<lsp::Client> cli = lsp::NewClient(hostport, prm, &err);
+  if (!cli) {
+    printf("Failed to join with server: %s\n", err.c_str());
+    return 1;
+  }
+  if (!cli->Write(bitcoin::Marshal(bitcoin::NewJoin()), &err)) {
+    cli->Close();
+    printf("Failed to join with server: %s\n", err.c_str());
+    return 1;
+  }
+  for (;;) {
+    std::string buf;
+    if (!cli->Read(&buf)) break;
+    bitcoin::Message req;
+    if (!bitcoin::Unmarshal(buf, &req)) req = bitcoin::Message();  // miner.go:54-55 ignores the error
+    const bitcoin::Message res = miner::HandleRequest(req, chunk);
+    if (!cli->Write(bitcoin::Marshal(res))) break;
+  }
+  cli->Close();  // miner.go:47 (defer miner.Close())
+  p1hip_shutdown();
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) return usage();
   const std::string cmd = argv[1];
+  lspnet::ConfigureFromEnv();
   try {
+    if (cmd == "lsp" && argc >= 3) return run_lsp(argc, argv);
     if (cmd == "scan" && argc == 5) {
       uint64_t lo, hi, h, n;
       if (!parse_u64(argv[3], &lo) || !parse_u64(argv[4], &hi)) return usage();

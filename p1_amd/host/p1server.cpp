@@ -1,34 +1,28 @@
-// p1server -- job splitting, scheduling and result aggregation across
-// GPU-backed miner processes (configs[4] without the
-// LSP transport).
+// p1server -- the bitcoin server: splits client requests into chunks,
+// schedules them over GPU-backed miners and returns each client the min
+// (hash, nonce) of its range (configs[4]).
 //
 // Reference: /root/reference/src/github.com/cmu440/bitcoin/server/server.go
-//   :119-140  a client Request goes, unsplit, to the first idle miner
-//   :141-152  a miner's Result is forwarded to the client
-//   :86-115   a lost miner's job should be reassigned (buggy there)
-// The handout (p1.pdf 4.2) asks the server to split a request over the
-// miners and to reassign the work of a miner that is lost.  Here:
-//   * each client request [Lower, Upper] is cut into chunks of `chunk` nonces;
-//   * chunks are dealt to idle miners, round-robin over the pending requests
-//     (a small request is not starved behind a large one);
-//   * a miner is a child process ("p1miner serve --device D" by default)
-//     speaking newline-delimited encoding/json bitcoin.Message on its
-//     stdin/stdout -- the same bytes the reference carries in LSP payloads;
-//   * when a miner's pipe closes, its in-flight chunk goes back to the front
-//     of its request's queue and the miner is dropped;
-//   * a request's result is the lexicographic (hash, nonce) min over its
-//     chunks with miner.go:56's identity, which equals the single-miner scan.
+// (job policy: scheduler.hpp).  Two transports, one scheduler:
 //
-// usage:
-//   p1server [opts] scan <msg> <lower> <upper>   one request; prints
-//                                                "Result <hash> <nonce>"
-//   p1server [opts] serve                        one JSON Request per stdin
-//                                                line -> one JSON Result line
-//                                                per request, in request order
-// opts: --miners N (default 1)  --devices d0,d1,..  (device of miner i =
-//       devices[i % len]; default 0)  --chunk C (default 2^32)
-//       --miner-cmd "CMD"  (a shell command run per miner; "{dev}" is replaced
-//       by the miner's device; default: <dir of p1server>/p1miner serve --device {dev})
+//   p1server [opts] lsp <port>                    server.go:45-170 over LSP/UDP:
+//       prints "Server listening on port P" (port 0 picks one, server.go:79);
+//       miners connect with `p1miner lsp host:port` and send Join, clients with
+//       `p1client host:port msg maxNonce` send a Request; every message is the
+//       encoding/json bitcoin.Message in an LSP payload.  A lost miner's chunk
+//       is re-queued, a lost client's request dropped.  --exit-after N: exit 0
+//       after answering N requests (tests, benchmarks); otherwise runs forever.
+//   p1server [opts] scan <msg> <lower> <upper>    one request over child-process
+//       miners ("p1miner serve" on pipes); prints "Result <hash> <nonce>"
+//   p1server [opts] serve                         JSON Requests on stdin -> JSON
+//       Results on stdout, in request order, over child-process miners
+//
+// opts: --chunk C (nonces per miner job, default 2^32)
+//   lsp:   --epoch-limit K --epoch-millis M --window W (lsp.Params; default
+//          NewParams(): 5, 2000, 1).  P1LSP_* env vars inject loss (lspnet.hpp).
+//   pipes: --miners N (default 1)  --devices d0,d1,.. (device of miner i =
+//          devices[i % len]; default 0)  --miner-cmd "CMD" (shell command per
+//          miner, "{dev}" -> its device; default <dir>/p1miner serve --device {dev})
 #include <errno.h>
 #include <fcntl.h>
 #include <inttypes.h>
@@ -40,38 +34,70 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
-#include <deque>
 #include <iostream>
 #include <map>
 #include <string>
 #include <vector>
 
 #include "bitcoin.hpp"
+#include "lsp.hpp"
+#include "lspnet.hpp"
+#include "scheduler.hpp"
 
 namespace {
 
-struct Chunk {
-  uint64_t req;  // request id
-  uint64_t lo, hi;
-};
+// ----------------------------------------------------------------------------
+// LSP transport (server.go:83-168)
+// ----------------------------------------------------------------------------
+int run_lsp(int port, const lsp::Params& prm, uint64_t chunk, long exit_after) {
+  std::string err;
+  std::unique_ptr<lsp::Server> srv = lsp::NewServer(port, prm, &err);
+  if (!srv) {
+    printf("%s\n", err.c_str());
+    return 1;
+  }
+  printf("Server listening on port %d\n", srv->Port());
+  fflush(stdout);
+  sched::Scheduler S(chunk);
+  long answered = 0;
+  for (;;) {
+    int id = 0;
+    std::string payload;
+    if (!srv->Read(&id, &payload, &err)) {
+      if (id == 0) return 1;  // server closed
+      // a lost connection: a miner's chunk is re-queued, a client's request dropped
+      if (S.IsMiner(id)) S.LoseMiner(id);
+      else S.CancelClient(id);
+    } else {
+      bitcoin::Message m;
+      if (bitcoin::Unmarshal(payload, &m)) {
+        switch (m.Type) {
+          case bitcoin::Join: S.AddMiner(id); break;
+          case bitcoin::Request: S.Submit(id, m.Data, m.Lower, m.Upper); break;
+          case bitcoin::Result: S.Result(id, m.Hash, m.Nonce); break;
+        }
+      }
+    }
+    for (const sched::Assignment& a : S.Dispatch())
+      if (!srv->Write(a.miner, bitcoin::Marshal(bitcoin::NewRequest(a.data, a.lo, a.hi)))) S.Unassign(a.miner);
+    for (const sched::Done& d : S.TakeDone()) {
+      srv->Write((int)d.client, bitcoin::Marshal(bitcoin::NewResult(d.hash, d.nonce)));  // client may be gone
+      if (exit_after > 0 && ++answered >= exit_after) {
+        srv->Close();  // blocks until the results are acknowledged
+        return 0;
+      }
+    }
+  }
+}
 
-struct Req {
-  uint64_t id;
-  std::string data;
-  std::deque<Chunk> todo;  // not yet assigned
-  uint64_t outstanding = 0;
-  uint64_t best = UINT64_MAX, best_n = 0;
-  bool found = false;
-};
-
-struct Miner {
+// ----------------------------------------------------------------------------
+// Child-process transport: each miner is "p1miner serve" on a pipe pair,
+// speaking newline-delimited encoding/json bitcoin.Message.
+// ----------------------------------------------------------------------------
+struct Child {
   pid_t pid = -1;
-  int in_fd = -1;   // we write requests here
-  int out_fd = -1;  // we read results here
+  int in_fd = -1, out_fd = -1;
   std::string buf;
-  bool busy = false;
-  Chunk cur{};
-  bool alive = true;
 };
 
 std::string dir_of_self() {
@@ -84,7 +110,7 @@ std::string dir_of_self() {
   return k == std::string::npos ? "." : s.substr(0, k);
 }
 
-bool spawn(Miner& m, const std::string& cmd) {
+bool spawn(Child& m, const std::string& cmd) {
   int in_p[2], out_p[2];
   if (pipe(in_p) || pipe(out_p)) return false;
   pid_t pid = fork();
@@ -104,11 +130,10 @@ bool spawn(Miner& m, const std::string& cmd) {
   return true;
 }
 
-void kill_miner(Miner& m) {
+void reap(Child& m) {
   if (m.in_fd >= 0) close(m.in_fd);
   if (m.out_fd >= 0) close(m.out_fd);
   m.in_fd = m.out_fd = -1;
-  m.alive = false;
   if (m.pid > 0) {
     int st;
     if (waitpid(m.pid, &st, WNOHANG) == 0) {
@@ -132,70 +157,55 @@ bool write_all(int fd, const std::string& s) {
   return true;
 }
 
-class Server {
+class PipeServer {
  public:
-  Server(int nminers, std::vector<int> devs, uint64_t chunk, std::string cmd)
-      : chunk_(chunk ? chunk : (1ull << 32)) {
-    const std::string def = dir_of_self() + "/p1miner serve --device {dev}";
-    if (cmd.empty()) cmd = def;
+  PipeServer(int nminers, std::vector<int> devs, uint64_t chunk, std::string cmd) : S_(chunk) {
+    if (cmd.empty()) cmd = dir_of_self() + "/p1miner serve --device {dev}";
     for (int i = 0; i < nminers; ++i) {
-      Miner m;
+      Child m;
       std::string c = cmd;
       const int dev = devs.empty() ? 0 : devs[i % devs.size()];
       for (size_t k; (k = c.find("{dev}")) != std::string::npos;) c.replace(k, 5, std::to_string(dev));
       if (!spawn(m, c)) { fprintf(stderr, "p1server: cannot start miner %d\n", i); continue; }
-      miners_.push_back(m);
+      kids_[i] = m;
+      S_.AddMiner(i);
     }
   }
-  ~Server() {
-    for (Miner& m : miners_) kill_miner(m);
+  ~PipeServer() {
+    for (auto& kv : kids_) reap(kv.second);
   }
+  size_t miners() const { return S_.Miners(); }
+  uint64_t submit(const std::string& data, uint64_t lo, uint64_t hi) { return S_.Submit(0, data, lo, hi); }
 
-  // Queue a client request (server.go:119-140, with splitting).
-  uint64_t submit(const std::string& data, uint64_t lo, uint64_t hi) {
-    Req r;
-    r.id = next_id_++;
-    r.data = data;
-    if (lo <= hi) {
-      for (uint64_t a = lo;;) {
-        const uint64_t b = (hi - a >= chunk_) ? a + (chunk_ - 1) : hi;
-        r.todo.push_back({r.id, a, b});
-        if (b == hi) break;
-        a = b + 1;
-      }
-    }
-    const uint64_t id = r.id;
-    order_.push_back(id);
-    reqs_[id] = std::move(r);
-    return id;
-  }
-
-  // Run until every submitted request is answered; calls done(id, hash, nonce)
-  // in completion order.  Returns false if every miner is lost with work left.
+  // Run until every request is answered; done(id, hash, nonce) in completion
+  // order.  false if every miner is lost with work left.
   template <typename F>
   bool run(F done) {
     for (;;) {
-      finish_empty(done);
-      if (reqs_.empty()) return true;
-      dispatch();
+      for (const sched::Done& d : S_.TakeDone()) done(d.req, d.hash, d.nonce);
+      if (S_.Idle()) return true;
+      for (const sched::Assignment& a : S_.Dispatch()) {
+        const std::string line = bitcoin::Marshal(bitcoin::NewRequest(a.data, a.lo, a.hi)) + "\n";
+        if (!write_all(kids_[a.miner].in_fd, line)) lose(a.miner);
+      }
+      if (S_.Starved()) return false;
       std::vector<pollfd> pf;
-      std::vector<size_t> who;
-      for (size_t i = 0; i < miners_.size(); ++i)
-        if (miners_[i].alive) { pf.push_back({miners_[i].out_fd, POLLIN, 0}); who.push_back(i); }
-      if (pf.empty()) return false;
+      std::vector<int> who;
+      for (auto& kv : kids_) {
+        pf.push_back({kv.second.out_fd, POLLIN, 0});
+        who.push_back(kv.first);
+      }
       if (poll(pf.data(), pf.size(), -1) < 0) {
         if (errno == EINTR) continue;
         return false;
       }
       for (size_t k = 0; k < pf.size(); ++k) {
         if (!(pf[k].revents & (POLLIN | POLLHUP | POLLERR))) continue;
-        Miner& m = miners_[who[k]];
+        Child& m = kids_[who[k]];
         char tmp[4096];
         ssize_t n = read(m.out_fd, tmp, sizeof tmp);
-        if (n <= 0) {  // miner lost: reassign its chunk (server.go:86-115 intent)
-          if (m.busy) requeue(m.cur);
-          m.busy = false;
-          kill_miner(m);
+        if (n <= 0) {  // miner lost: its chunk is re-queued (server.go:86-115 intent)
+          lose(who[k]);
           continue;
         }
         m.buf.append(tmp, (size_t)n);
@@ -204,97 +214,30 @@ class Server {
           std::string line = m.buf.substr(0, nl);
           m.buf.erase(0, nl + 1);
           bitcoin::Message res;
-          if (!m.busy || !bitcoin::Unmarshal(line, &res) || res.Type != bitcoin::Result) continue;
-          m.busy = false;
-          merge(m.cur, res.Hash, res.Nonce);
+          if (bitcoin::Unmarshal(line, &res) && res.Type == bitcoin::Result) S_.Result(who[k], res.Hash, res.Nonce);
         }
       }
     }
-  }
-
-  size_t live_miners() const {
-    size_t n = 0;
-    for (const Miner& m : miners_) n += m.alive ? 1 : 0;
-    return n;
   }
 
  private:
-  void requeue(const Chunk& c) {
-    auto it = reqs_.find(c.req);
-    if (it == reqs_.end()) return;
-    it->second.outstanding--;
-    it->second.todo.push_front(c);
-  }
-
-  void merge(const Chunk& c, uint64_t h, uint64_t n) {
-    auto it = reqs_.find(c.req);
-    if (it == reqs_.end()) return;
-    Req& r = it->second;
-    r.outstanding--;
-    // a chunk whose hashes are all MaxUint64 reports (Max, 0); only real
-    // minima (< Max) take part, lexicographically -- identity of miner.go:56
-    if (h < UINT64_MAX && (!r.found || h < r.best || (h == r.best && n < r.best_n))) {
-      r.best = h;
-      r.best_n = n;
-      r.found = true;
+  void lose(int miner) {
+    S_.LoseMiner(miner);
+    auto it = kids_.find(miner);
+    if (it != kids_.end()) {
+      reap(it->second);
+      kids_.erase(it);
     }
   }
 
-  // Round-robin over requests with pending chunks, one chunk per idle miner.
-  void dispatch() {
-    for (Miner& m : miners_) {
-      if (!m.alive || m.busy) continue;
-      bool any = false;
-      for (size_t tries = 0; tries < order_.size(); ++tries) {
-        const uint64_t id = order_[rr_++ % order_.size()];
-        auto it = reqs_.find(id);
-        if (it == reqs_.end() || it->second.todo.empty()) continue;
-        Req& r = it->second;
-        Chunk c = r.todo.front();
-        r.todo.pop_front();
-        r.outstanding++;
-        const std::string line = bitcoin::Marshal(bitcoin::NewRequest(r.data, c.lo, c.hi)) + "\n";
-        if (!write_all(m.in_fd, line)) {
-          r.outstanding--;
-          r.todo.push_front(c);
-          kill_miner(m);
-        } else {
-          m.busy = true;
-          m.cur = c;
-        }
-        any = true;
-        break;
-      }
-      if (!any) break;
-    }
-  }
-
-  template <typename F>
-  void finish_empty(F& done) {
-    for (auto it = reqs_.begin(); it != reqs_.end();) {
-      Req& r = it->second;
-      if (r.todo.empty() && r.outstanding == 0) {
-        done(r.id, r.found ? r.best : UINT64_MAX, r.found ? r.best_n : 0);
-        for (size_t i = 0; i < order_.size(); ++i)
-          if (order_[i] == r.id) { order_.erase(order_.begin() + i); break; }
-        it = reqs_.erase(it);
-      } else {
-        ++it;
-      }
-    }
-  }
-
-  uint64_t chunk_;
-  std::vector<Miner> miners_;
-  std::map<uint64_t, Req> reqs_;
-  std::vector<uint64_t> order_;
-  size_t rr_ = 0;
-  uint64_t next_id_ = 1;
+  sched::Scheduler S_;
+  std::map<int, Child> kids_;
 };
 
 int usage() {
   fprintf(stderr,
-          "usage: p1server [--miners N] [--devices d0,d1,..] [--chunk C] [--miner-cmd CMD] "
+          "usage: p1server [--chunk C] [--epoch-limit K] [--epoch-millis M] [--window W] [--exit-after N] lsp <port>\n"
+          "       p1server [--chunk C] [--miners N] [--devices d0,d1,..] [--miner-cmd CMD] "
           "scan <msg> <lower> <upper> | serve\n");
   return 2;
 }
@@ -313,10 +256,13 @@ bool parse_u64(const char* s, uint64_t* v) {
 
 int main(int argc, char** argv) {
   signal(SIGPIPE, SIG_IGN);
+  lspnet::ConfigureFromEnv();
   int nminers = 1;
   std::vector<int> devs;
   uint64_t chunk = 1ull << 32;
   std::string cmd;
+  lsp::Params prm = lsp::NewParams();
+  long exit_after = 0;
   int i = 1;
   for (; i < argc; ++i) {
     if (!strcmp(argv[i], "--miners") && i + 1 < argc) nminers = atoi(argv[++i]);
@@ -331,12 +277,26 @@ int main(int argc, char** argv) {
     } else if (!strcmp(argv[i], "--chunk") && i + 1 < argc) {
       if (!parse_u64(argv[++i], &chunk) || chunk == 0) return usage();
     } else if (!strcmp(argv[i], "--miner-cmd") && i + 1 < argc) cmd = argv[++i];
+    else if (!strcmp(argv[i], "--epoch-limit") && i + 1 < argc) prm.EpochLimit = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--epoch-millis") && i + 1 < argc) prm.EpochMillis = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--window") && i + 1 < argc) prm.WindowSize = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--exit-after") && i + 1 < argc) exit_after = atol(argv[++i]);
     else break;
   }
-  if (i >= argc || nminers < 1) return usage();
+  if (i >= argc || nminers < 1 || prm.EpochLimit < 1 || prm.EpochMillis < 1 || prm.WindowSize < 1) return usage();
   const std::string mode = argv[i];
-  Server srv(nminers, devs, chunk, cmd);
-  if (srv.live_miners() == 0) { fprintf(stderr, "p1server: no miner started\n"); return 1; }
+  if (mode == "lsp" && i + 2 == argc) {
+    char* end = nullptr;
+    const long port = strtol(argv[i + 1], &end, 10);
+    if (*end || port < 0 || port > 65535) {
+      printf("Port must be a number: %s\n", argv[i + 1]);  // server.go:68-72
+      return 1;
+    }
+    return run_lsp((int)port, prm, chunk, exit_after);
+  }
+  if (mode != "scan" && mode != "serve") return usage();
+  PipeServer srv(nminers, devs, chunk, cmd);
+  if (srv.miners() == 0) { fprintf(stderr, "p1server: no miner started\n"); return 1; }
   if (mode == "scan" && i + 4 == argc) {
     uint64_t lo, hi;
     if (!parse_u64(argv[i + 2], &lo) || !parse_u64(argv[i + 3], &hi)) return usage();

@@ -1,0 +1,206 @@
+// scheduler.hpp -- the bitcoin server's job bookkeeping, independent of the
+// transport that carries requests and results (LSP connections in
+// `p1server lsp`, child-process pipes in `p1server scan|serve`).
+//
+// Reference: /root/reference/src/github.com/cmu440/bitcoin/server/server.go
+//   :119-140  a client Request is handed, unsplit, to the first idle miner
+//   :141-152  a miner's Result is forwarded to the requesting client
+//   :86-115   a lost miner's job should go to another miner (buggy there:
+//             it writes to the lost connection and re-queues the job twice)
+//   :153-167  a Join makes a miner idle and hands it the oldest queued job
+// The handout (p1.pdf 4.2) asks the server to split large requests over the
+// miners, to schedule fairly and to survive miner and client loss.  Here:
+//   * a request [Lower, Upper] becomes chunks of at most `chunk` nonces;
+//   * idle miners take chunks round-robin over the open requests, so a small
+//     request is not starved behind a large one;
+//   * a lost miner's chunk goes back to the front of its request's queue;
+//   * a lost client's requests are dropped (results of their chunks still in
+//     flight are ignored when they arrive);
+//   * a request's answer is the lexicographic (hash, nonce) min over its
+//     chunks with miner.go:56's identity (MaxUint64, 0) -- identical to one
+//     miner scanning the whole range (contiguous chunks, strict '<').
+#pragma once
+#include <stdint.h>
+
+#include <deque>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace sched {
+
+struct Assignment {
+  int miner;
+  uint64_t req;
+  std::string data;
+  uint64_t lo, hi;
+};
+
+struct Done {
+  uint64_t req;
+  int64_t client;  // transport key of the requester
+  uint64_t hash, nonce;
+};
+
+class Scheduler {
+ public:
+  explicit Scheduler(uint64_t chunk) : chunk_(chunk ? chunk : (1ull << 32)) {}
+
+  // A client request (server.go:119-140, with splitting).  Returns its id.
+  uint64_t Submit(int64_t client, const std::string& data, uint64_t lo, uint64_t hi) {
+    Req r;
+    r.id = next_id_++;
+    r.client = client;
+    r.data = data;
+    if (lo <= hi) {
+      for (uint64_t a = lo;;) {
+        const uint64_t b = (hi - a >= chunk_) ? a + (chunk_ - 1) : hi;
+        r.todo.push_back({a, b});
+        if (b == hi) break;
+        a = b + 1;
+      }
+    }
+    order_.push_back(r.id);
+    const uint64_t id = r.id;
+    reqs_.emplace(id, std::move(r));
+    return id;
+  }
+
+  // The requester's connection is gone: forget its requests.
+  void CancelClient(int64_t client) {
+    for (auto it = reqs_.begin(); it != reqs_.end();) {
+      if (it->second.client == client) {
+        drop_order(it->first);
+        it = reqs_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+
+  void AddMiner(int miner) { miners_[miner]; }  // idle (server.go:153-166)
+  bool IsMiner(int miner) const { return miners_.count(miner) != 0; }
+  size_t Miners() const { return miners_.size(); }
+
+  // A miner is lost: its chunk goes back to the front of its request.
+  void LoseMiner(int miner) {
+    auto it = miners_.find(miner);
+    if (it == miners_.end()) return;
+    if (it->second.busy) requeue(it->second.cur_req, it->second.lo, it->second.hi);
+    miners_.erase(it);
+  }
+
+  // A miner's Result for its current chunk.  Returns false if the miner had
+  // no chunk (a stray Result is ignored).
+  bool Result(int miner, uint64_t hash, uint64_t nonce) {
+    auto it = miners_.find(miner);
+    if (it == miners_.end() || !it->second.busy) return false;
+    Miner& m = it->second;
+    m.busy = false;
+    auto r = reqs_.find(m.cur_req);
+    if (r == reqs_.end()) return true;  // its client is gone
+    Req& q = r->second;
+    q.outstanding--;
+    // a chunk whose hashes are all MaxUint64 reports (Max, 0); only real
+    // minima (< Max) take part, lexicographically -- identity of miner.go:56
+    if (hash < UINT64_MAX && (!q.found || hash < q.best || (hash == q.best && nonce < q.best_n))) {
+      q.best = hash;
+      q.best_n = nonce;
+      q.found = true;
+    }
+    return true;
+  }
+
+  // Hand one chunk to every idle miner, round-robin over open requests.
+  std::vector<Assignment> Dispatch() {
+    std::vector<Assignment> out;
+    for (auto& kv : miners_) {
+      Miner& m = kv.second;
+      if (m.busy) continue;
+      bool any = false;
+      for (size_t tries = 0; tries < order_.size(); ++tries) {
+        const uint64_t id = order_[rr_++ % order_.size()];
+        auto it = reqs_.find(id);
+        if (it == reqs_.end() || it->second.todo.empty()) continue;
+        Req& r = it->second;
+        const Span c = r.todo.front();
+        r.todo.pop_front();
+        r.outstanding++;
+        m.busy = true;
+        m.cur_req = id;
+        m.lo = c.lo;
+        m.hi = c.hi;
+        out.push_back({kv.first, id, r.data, c.lo, c.hi});
+        any = true;
+        break;
+      }
+      if (!any) break;
+    }
+    return out;
+  }
+
+  // A chunk could not be sent (the miner's connection failed): undo it and
+  // drop the miner.
+  void Unassign(int miner) { LoseMiner(miner); }
+
+  // Requests whose chunks are all answered, in completion order.
+  std::vector<Done> TakeDone() {
+    std::vector<Done> out;
+    for (auto it = reqs_.begin(); it != reqs_.end();) {
+      Req& r = it->second;
+      if (r.todo.empty() && r.outstanding == 0) {
+        out.push_back({r.id, r.client, r.found ? r.best : UINT64_MAX, r.found ? r.best_n : 0});
+        drop_order(r.id);
+        it = reqs_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    return out;
+  }
+
+  bool Idle() const { return reqs_.empty(); }
+  // Work is waiting but no miner could take it.
+  bool Starved() const { return !reqs_.empty() && miners_.empty(); }
+
+ private:
+  struct Span {
+    uint64_t lo, hi;
+  };
+  struct Req {
+    uint64_t id;
+    int64_t client;
+    std::string data;
+    std::deque<Span> todo;
+    uint64_t outstanding = 0;
+    uint64_t best = UINT64_MAX, best_n = 0;
+    bool found = false;
+  };
+  struct Miner {
+    bool busy = false;
+    uint64_t cur_req = 0, lo = 0, hi = 0;
+  };
+
+  void requeue(uint64_t req, uint64_t lo, uint64_t hi) {
+    auto it = reqs_.find(req);
+    if (it == reqs_.end()) return;
+    it->second.outstanding--;
+    it->second.todo.push_front({lo, hi});
+  }
+  void drop_order(uint64_t id) {
+    for (size_t i = 0; i < order_.size(); ++i)
+      if (order_[i] == id) {
+        order_.erase(order_.begin() + i);
+        return;
+      }
+  }
+
+  uint64_t chunk_;
+  std::map<int, Miner> miners_;
+  std::map<uint64_t, Req> reqs_;
+  std::vector<uint64_t> order_;
+  size_t rr_ = 0;
+  uint64_t next_id_ = 1;
+};
+
+}  // namespace sched

@@ -66,20 +66,23 @@ def test_cli_scan_config1():
 @pytest.mark.gpu
 def test_cli_serve_loop(oracle_mod):
     reqs = [
-        {"Type": 0, "Data": "", "Lower": 0, "Upper": 0, "Hash": 0, "Nonce": 0},    # Join: ignored
+        {"Type": 0, "Data": "", "Lower": 0, "Upper": 0, "Hash": 0, "Nonce": 0},    # Join: scanned like any line
         {"Type": 1, "Data": "bradfitz", "Lower": 0, "Upper": 9999, "Hash": 0, "Nonce": 0},
         {"Type": 1, "Data": "msg", "Lower": 0, "Upper": 2, "Hash": 0, "Nonce": 0},
         {"Type": 1, "Data": "héllo", "Lower": 10**9 - 3000, "Upper": 10**9 + 3000, "Hash": 0, "Nonce": 0},
         {"Type": 1, "Data": "x", "Lower": 9, "Upper": 3, "Hash": 0, "Nonce": 0},
     ]
-    stdin = "\n".join(json.dumps(r, ensure_ascii=False) for r in reqs) + "\n"
+    # miner.go:49-67 answers every message it reads: it decodes into a zero
+    # Message (errors ignored) and scans [Lower, Upper] whatever the Type; an
+    # undecodable line is the request ("", [0, 0])
+    stdin = "\n".join(json.dumps(r, ensure_ascii=False) for r in reqs) + "\nnot json\n"
     r = run(["serve", "--device", "0", "--chunk", "1000"], stdin)  # small chunks: exercises chunking
     assert r.returncode == 0, r.stderr
     res = [json.loads(x) for x in r.stdout.splitlines()]
-    assert len(res) == 4 and all(x["Type"] == 2 for x in res)
-    want = [oracle_mod.scan(q["Data"], q["Lower"], q["Upper"], threads=8) for q in reqs[1:]]
+    assert len(res) == 6 and all(x["Type"] == 2 for x in res)
+    want = [oracle_mod.scan(q["Data"], q["Lower"], q["Upper"], threads=8) for q in reqs] + [oracle_mod.scan("", 0, 0)]
     assert [(x["Hash"], x["Nonce"]) for x in res] == want
-    assert want[-1] == (U64_MAX, 0)
+    assert want[-2] == (U64_MAX, 0)
 
 
 def test_lsp_message_wire_format_matches_go():

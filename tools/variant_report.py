@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Per-variant report of the fast scan kernel: for every (FV, NV, TRAIL) of
+p1_amd/csrc/fast_variants.inc, build k_scan with only that variant through
+the shipped pipeline (hipcc -S -> tools/isa_post.py -> code object) and read
+
+  * .vgpr_count / .sgpr_count / .sgpr_spill_count and the waves per SIMD
+    they admit (VGPR: 512 / vgprs; SGPR: MI355X_MICROARCH.md:225-226,
+    blocks of 256 threads per CU = floor(800 / (ceil(sgpr/16)*16 + 16)));
+  * the innermost per-nonce loop (largest loop containing no other loop):
+    VALU instructions by issue class -- half-rate "A" (v_alignbit_b32,
+    v_add3_u32 and the other 3-input VOP3 integer ops) and full-rate "B" --
+    SALU instructions, bytes, and how many 8-byte instructions sit at
+    4 (mod 8);
+  * a predicted rate from the measured issue costs (A 4.37,
+    B 2.66 SIMD cycles per wave instruction at 4 waves/SIMD) at 2.35 GHz.
+
+usage: variant_report.py [--jobs N] [--only FV,NV,TR ...] [--waves W] > out.jsonl
+"""
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = "/opt/rocm/bin/hipcc"
+LLVM = "/opt/rocm/lib/llvm/bin"
+HALF_RATE = {"v_alignbit_b32", "v_add3_u32", "v_alignbyte_b32", "v_perm_b32", "v_xad_u32", "v_or3_b32",
+             "v_lshl_or_b32", "v_lshl_add_u32", "v_add_lshl_u32", "v_and_or_b32", "v_bfi_b32", "v_bfe_u32",
+             "v_mad_u32_u24", "v_pk_add_u16", "v_cndmask_b32_e64"}
+COST_A, COST_B, CLOCK = 4.37, 2.66, 2.35e9
+
+
+def variants():
+    out = []
+    for ln in open(os.path.join(ROOT, "p1_amd/csrc/fast_variants.inc")):
+        m = re.match(r"P1_CASE\((\d+),\s*(\d+),\s*(true|false)\)", ln)
+        if m:
+            out.append((int(m.group(1)), int(m.group(2)), m.group(3) == "true"))
+    return out
+
+
+def meta(s_text, kern="k_scan"):
+    i = s_text.find(f".name:           {kern}\n")
+    blk = s_text[i:i + 2000]
+    get = lambda k: int(re.search(rf"\.{k}:\s+(\d+)", blk).group(1))
+    return {"vgpr": get("vgpr_count"), "sgpr": get("sgpr_count"), "sgpr_spill": get("sgpr_spill_count"),
+            "vgpr_spill": get("vgpr_spill_count")}
+
+
+def loops_of(co, kern="k_scan"):
+    dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", co], capture_output=True,
+                         text=True).stdout.split("\n")
+    ins, on = [], False
+    for ln in dis:
+        mh = re.match(r"^([0-9a-f]+) <(.*)>:", ln)
+        if mh:
+            on = mh.group(2) == kern
+            continue
+        m = re.search(r"^\s+(\S.*?)\s*//\s*([0-9A-Fa-f]+):\s*((?:[0-9A-Fa-f]{8}\s*)+)(<.*>)?$", ln)
+        if on and m:
+            ins.append((int(m.group(2), 16), 4 * len(m.group(3).split()), m.group(1)))
+    loops = []
+    for a, sz, t in ins:
+        m = re.match(r"s_cbranch_\w+\s+(\d+)", t)
+        if m:
+            off = int(m.group(1))
+            off = off - 65536 if off >= 32768 else off
+            tgt = a + 4 + 4 * off
+            if tgt < a:
+                loops.append((tgt, a))
+    inner = [l for l in loops if not any(o != l and l[0] <= o[0] and o[1] <= l[1] for o in loops)]
+    return ins, inner
+
+
+def mix(ins, lo, hi):
+    body = [(a, sz, t) for a, sz, t in ins if lo <= a <= hi]
+    A = B = S = other = n8 = at4 = 0
+    for a, sz, t in body:
+        op = t.split()[0]
+        if sz == 8:
+            n8 += 1
+            at4 += a % 8 == 4
+        if op.startswith("v_"):
+            if op in HALF_RATE:
+                A += 1
+            else:
+                B += 1
+        elif op.startswith("s_"):
+            S += 1
+        else:
+            other += 1
+    cyc = A * COST_A + B * COST_B
+    return {"valu": A + B, "half_rate_A": A, "full_rate_B": B, "salu": S, "other": other, "bytes": hi - lo + 4,
+            "n8": n8, "n8_at_4_mod_8": at4, "pred_simd_cycles_per_wave_iter": cyc,
+            "pred_GH_s": 1024 * CLOCK * 64 / cyc / 1e9 if cyc else None}
+
+
+def build_one(v, waves, isapost):
+    fv, nv, tr = v
+    with tempfile.TemporaryDirectory() as td:
+        inc = os.path.join(td, "v.inc")
+        open(inc, "w").write(f"P1_CASE({fv}, {nv}, {'true' if tr else 'false'})\n")
+        s = os.path.join(td, "k.s")
+        cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S", "-o", s,
+               f"-DP1_VARIANTS_INC=\"{inc}\"", os.path.join(ROOT, "p1_amd/csrc/p1hip_kernels.hip")]
+        if waves:
+            cmd.insert(1, f"-DP1_FAST_WAVES={waves}")
+        subprocess.run(cmd, check=True, capture_output=True)
+        post = os.path.join(td, "k.post.s")
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools/isa_post.py"), s, post] + isapost, check=True,
+                       capture_output=True)
+        o, co = os.path.join(td, "k.o"), os.path.join(td, "k.co")
+        subprocess.run([f"{LLVM}/clang", "-cc1as", "-triple", "amdgcn-amd-amdhsa", "-filetype", "obj", "-target-cpu",
+                        "gfx950", "-mrelocation-model", "pic", "-o", o, post], check=True)
+        subprocess.run([f"{LLVM}/ld.lld", "-m", "elf64_amdgpu", "--no-undefined", "-shared", "-o", co, o], check=True)
+        r = {"variant": [fv, nv, tr]}
+        r.update(meta(open(s).read()))
+        ins, inner = loops_of(co)
+        big = max(inner, key=lambda l: l[1] - l[0])
+        r["loop"] = mix(ins, *big)
+        r["waves_per_simd_vgpr"] = min(8, 512 // max(1, r["vgpr"]))
+        r["blocks_per_cu_sgpr"] = min(8, 800 // ((-(-r["sgpr"] // 16)) * 16 + 16))
+        return r
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=8)
+    ap.add_argument("--only", nargs="*", default=None)
+    ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--isapost", default="--align-loops=3 --loop-offset=4 --loop-parity")
+    a = ap.parse_args()
+    vs = variants()
+    if a.only:
+        want = {tuple(int(x) if x.isdigit() else x == "true" for x in o.split(",")) for o in a.only}
+        vs = [v for v in vs if v in want]
+    with cf.ThreadPoolExecutor(a.jobs) as ex:
+        for r in ex.map(lambda v: build_one(v, a.waves, a.isapost.split()), vs):
+            r["waves_build"] = a.waves or 4
+            print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
