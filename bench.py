@@ -72,6 +72,13 @@ CONFIGS = {
 ALG_MIX = {"v_alignbit_b32": 576, "v_bitop3_b32": 352, "v_add3_u32": 240, "v_add_u32": 120,
            "v_lshrrev_b32": 96}
 VALU_PEAK_PROFILE = "profiles/r01_valu_peak.jsonl"
+# Per-variant loop mix of the shipped kernel (tools/variant_report.py) and the
+# fastest measured single-class issue costs (SIMD cycles per wave instruction,
+# profiles/r01v_valu_runs.jsonl: v_alignbit_b32 / v_add3_u32 streams 4.23,
+# full-rate VOP2 streams 2.13): a loop of A half-rate and B full-rate
+# instructions cannot issue in fewer than A x 4.23 + B x 2.13 SIMD cycles.
+VARIANT_PROFILE = "profiles/r02_variant_report.jsonl"
+IDEAL_COST_A, IDEAL_COST_B = 4.23, 2.13
 
 
 class UsageError(SystemExit):
@@ -134,6 +141,50 @@ def mix_roofline():
     cu_cycles = sum(n / rate[k] for k, n in ALG_MIX.items())  # per nonce per compression
     return {"peak_GH_s_per_block": 256 * 2.4e9 / cu_cycles / 1e9, "cu_cycles_per_compression": cu_cycles,
             "rates_lane_ops_per_clk_cu": rate, "source": VALU_PEAK_PROFILE}
+
+
+def fast_variant(msg_len, d, k=3):
+    """(FV, NV, TRAIL) the planner picks for a d-digit decade of a message of
+    msg_len bytes at lo-digit count k (planner.hpp make_layout/add_fast)."""
+    r = (msg_len + 1) % 64
+    q = r + d - 1
+    nb = 1 if r + d + 9 <= 64 else 2
+    if nb == 1:
+        vb, trail = 0, False
+    elif q <= 63:
+        vb, trail = 0, True
+    elif q - 64 >= 2:
+        vb, trail = 1, False
+    else:
+        vb, trail, k = 1, False, q - 63
+    qv = q - 64 * vb
+    fv = (qv - k + 1) >> 2
+    return fv, (qv >> 2) - fv + 1, trail
+
+
+def workload_mix(msg_len, lo, hi):
+    """Nonce-weighted loop mix (half-rate A, full-rate B VALU instructions per
+    nonce) of the fast variants that scan [lo, hi]."""
+    path = os.path.join(ROOT, VARIANT_PROFILE)
+    if not os.path.exists(path):
+        return None
+    table = {}
+    for line in open(path):
+        d = json.loads(line)
+        table[tuple(d["variant"])] = d["loop"]
+    a = b = w = 0.0
+    for d in range(1, 21):
+        dlo, dhi = (0 if d == 1 else 10 ** (d - 1)), 10 ** d - 1
+        n = min(hi, dhi) - max(lo, dlo) + 1
+        if n <= 0 or d <= 3:
+            continue
+        v = table.get(fast_variant(msg_len, d))
+        if v is None:
+            return None
+        a += n * v["half_rate_A"]
+        b += n * v["full_rate_B"]
+        w += n
+    return (a / w, b / w) if w else None
 
 
 def pmc_summary(config):
@@ -334,14 +385,25 @@ def main():
                 "valu_instr_per_nonce": ipn,
                 "achieved": ipn * k_rate / 1e12,
                 "frac": ipn * k_rate / VALU_PEAK_OPS,
-                "issue_frac": pmc.get("issue_frac"),
                 "simd_cycles_per_valu_wave_instr": pmc.get("simd_cycles_per_valu_wave_instr"),
-                "valu_busy_frac": pmc.get("valu_busy_frac"),
+                "effective_clock_GHz": pmc.get("effective_clock_GHz"),
                 "source": pmc_src,
-                "note": "frac counts executed VALU lane-instructions against the same 78.6 T peak; "
-                        "issue_frac prices the executed mix at the measured per-class issue costs "
-                        "(half-rate alignbit/add3 vs full-rate ops, DESIGN.md 4)",
+                "note": "frac counts executed VALU lane-instructions against the same 78.6 T peak "
+                        "(SURVEY.md 8(d) accounting rule)",
             }
+            mix_ab = workload_mix(len(msg), 0, total - 1)
+            if mix_ab and k_rate > 0:
+                # the executed loop mix at its ideal issue rate vs the SIMD
+                # cycles this run spent per wave-iteration (64 nonces)
+                clk = (pmc.get("effective_clock_GHz") or 2.4) * 1e9
+                spent = 1024 * clk * 64 / k_rate
+                ideal = mix_ab[0] * IDEAL_COST_A + mix_ab[1] * IDEAL_COST_B
+                roofline["executed"]["mix_issue_frac"] = ideal / spent
+                roofline["executed"]["loop_mix_per_nonce"] = {"half_rate_A": mix_ab[0], "full_rate_B": mix_ab[1],
+                                                              "source": VARIANT_PROFILE}
+                roofline["executed"]["mix_issue_note"] = (
+                    "ideal SIMD cycles of the loop mix (A x 4.23 + B x 2.13, the fastest single-class "
+                    "issue costs measured by tools/valu_runs) / SIMD cycles spent per 64 nonces")
             if roofline["frac"] > 1.0:
                 roofline["executed"]["why_alg_frac_above_1"] = (
                     "the algorithmic count charges both tail blocks per nonce (SURVEY.md 8(d)); the kernel "

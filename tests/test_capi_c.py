@@ -40,3 +40,50 @@ def test_c_client_on_gpu(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip() == "Result 1419516646206828 9898"
+
+
+def _build_chunkloop(tmp_path):
+    exe = tmp_path / "capi_chunkloop"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror",
+                    "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "capi_chunkloop.c"),
+                    "-L", os.path.join(ROOT, "p1_amd"), "-lp1hip", f"-Wl,-rpath,{os.path.join(ROOT, 'p1_amd')}",
+                    "-L", os.path.join(ROOT, "oracle"), "-lp1oracle", f"-Wl,-rpath,{os.path.join(ROOT, 'oracle')}",
+                    "-o", str(exe)], check=True)
+    return str(exe)
+
+
+def test_chunkloop_builds_and_reports_no_device(tmp_path):
+    """INTEGRATION.md's chunk loop links as plain C; without a GPU the
+    library answers rc -1 (no CPU fallback inside the library)."""
+    exe = _build_chunkloop(tmp_path)
+    try:
+        import torch
+
+        if torch.cuda.device_count() > 0:
+            pytest.skip("GPU present: covered by test_chunkloop_on_gpu")
+    except ImportError:
+        pass
+    r = subprocess.run([exe, "bradfitz", "0", "9999", "1000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("nodevice"), r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_chunkloop_on_gpu(tmp_path, oracle_mod):
+    """The Go bridge's loop through the C ABI: chunked
+    scans equal one scan; the rc != 0 branch (an invalid argument on every
+    3rd chunk) falls back to the reference's CPU loop for that chunk and the
+    result is unchanged (miner.go:49-71)."""
+    exe = _build_chunkloop(tmp_path)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", "0").split(",")[0])
+    for msg, lo, hi, chunk in [("bradfitz", 0, 99999, 7919), ("msg", 0, 2, 1), ("x" * 70, 10**9 - 5000, 10**9 + 5000, 997)]:
+        want = oracle_mod.scan(msg, lo, hi, threads=8)
+        r = subprocess.run([exe, msg, str(lo), str(hi), str(chunk)], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert r.stdout.split()[:3] == ["Result", str(want[0]), str(want[1])], (msg, r.stdout)
+        assert "cpu_chunks=0" in r.stdout
+        r = subprocess.run([exe, msg, str(lo), str(hi), str(chunk), "3"], capture_output=True, text=True, timeout=300,
+                           env=env)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert r.stdout.split()[:3] == ["Result", str(want[0]), str(want[1])], (msg, r.stdout)
+        if (hi - lo + 1) // chunk >= 3:
+            assert "cpu_chunks=0" not in r.stdout

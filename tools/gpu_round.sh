@@ -19,7 +19,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 [ "${SKIP_PEAK:-0}" = 1 ] || step valu_peak 300 "$ROOT/tools/valu_peak" > "$OUT/${TAG}_valu_peak.jsonl"
 [ "${RUN_MIX:-0}" != 1 ] || step valu_mix 300 "$ROOT/tools/valu_mix" > "$OUT/${TAG}_valu_mix.jsonl"
-[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -u -m pytest "$ROOT/tests" -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/${TAG}_pytest_gpu.log" 2>&1
+[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -u -m pytest "$ROOT/tests" -m gpu -x -v -rP -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/${TAG}_pytest_gpu.log" 2>&1
 [ "${SKIP_SMOKE:-0}" = 1 ] || step smoke 300 python -c "import sys; sys.path.insert(0, '$ROOT'); import __graft_entry__ as g; g.smoke()" > "$OUT/${TAG}_smoke.log" 2>&1
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 600 python "$ROOT/bench.py" ${BENCH_ARGS:-} > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
 [ -z "${EXTRA_BENCH:-}" ] || step bench_extra 600 python "$ROOT/bench.py" $EXTRA_BENCH > "$OUT/${TAG}_bench_extra.json" 2> "$OUT/${TAG}_bench_extra.err"
