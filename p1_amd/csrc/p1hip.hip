@@ -240,14 +240,23 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
     return L.fast ? (uint64_t)L.fa.kpow * (uint64_t)L.btail : (uint64_t)L.btail - 1;
   };
   std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return weight(a) > weight(b); });
-  // pack into launches of <= kMaxSegs segments / kMaxLaunchBlocks workgroups
+  // Pack into launches of <= kMaxSegs segments / kMaxLaunchBlocks workgroups.
+  // When a scan needs several launches (e.g. configs[3]'s 2^38 nonces on one
+  // GPU), balance them: each batch closes once it reaches total/launches
+  // workgroups, so the launches are near-equal rather than one full and one
+  // small one (equal drains, and a per-launch average that means something).
   struct Batch { size_t first, count; uint32_t blocks; };
   std::vector<Batch> batches;
+  uint64_t all_blocks = 0;
+  for (const Launch& L : plan.launches) all_blocks += L.blocks;
+  const uint64_t nlaunch = (all_blocks + kMaxLaunchBlocks - 1) / kMaxLaunchBlocks;
+  const uint64_t target = nlaunch > 1 ? (all_blocks + nlaunch - 1) / nlaunch : kMaxLaunchBlocks;
   uint32_t total_blocks = 0;
   for (size_t r = 0; r < order.size(); ++r) {
     const Launch& L = plan.launches[order[r]];
-    if (batches.empty() || batches.back().count == kMaxSegs ||
-        batches.back().blocks + (uint64_t)L.blocks > kMaxLaunchBlocks)
+    const uint64_t cur = batches.empty() ? 0 : batches.back().blocks;
+    if (batches.empty() || batches.back().count == kMaxSegs || cur + (uint64_t)L.blocks > kMaxLaunchBlocks ||
+        (cur > 0 && cur + L.blocks / 2 > target && batches.size() < nlaunch))  // fits the next batch better
       batches.push_back({r, 0, 0});
     batches.back().count++;
     batches.back().blocks += L.blocks;
