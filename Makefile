@@ -68,15 +68,16 @@ tools/lsp_fake_miner: tests/lsp/lsp_fake_miner.cpp p1_amd/host/bitcoin.cpp $(HOS
 
 # host-only replay of the kernels' per-thread code (layout tests; not product)
 tools/p1emu: tools/p1emu.cpp $(HDRS)
-	$(HIPCC) -O2 -std=c++17 -o $@ tools/p1emu.cpp
+	$(HIPCC) -O2 -std=c++17 -DP1_NV2_PLAIN -o $@ tools/p1emu.cpp
 
 oracle:
 	$(MAKE) -C oracle
 
 # A/B tuning builds (not used unless P1HIP_LIB points at one):
 #   make variant NAME=x DEVEXTRA='-DP1_FAST_WAVES=5' ISAPOST='--no-e64'
+#   make variant NAME=nv2 DEVEXTRA=-DP1_NV2_PLAIN HOSTEXTRA=-DP1_NV2_PLAIN   (+ P1HIP_NO_SPLIT=1 at run time)
 variant:
-	$(MAKE) BUILD=build/var_$(NAME) DEVEXTRA="$(DEVEXTRA)" ISAPOST="$(ISAPOST)" build/var_$(NAME)/p1hip_kernels_blob.o build/var_$(NAME)/p1hip_host.o
+	$(MAKE) BUILD=build/var_$(NAME) DEVEXTRA="$(DEVEXTRA)" HIPFLAGS="$(HIPFLAGS) $(HOSTEXTRA)" ISAPOST="$(ISAPOST)" build/var_$(NAME)/p1hip_kernels_blob.o build/var_$(NAME)/p1hip_host.o
 	mkdir -p p1_amd/variants
 	$(HIPCC) -shared -fPIC -o p1_amd/variants/libp1hip_$(NAME).so build/var_$(NAME)/p1hip_host.o build/var_$(NAME)/p1hip_kernels_blob.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 

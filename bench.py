@@ -77,7 +77,7 @@ VALU_PEAK_PROFILE = "profiles/r01_valu_peak.jsonl"
 # profiles/r01v_valu_runs.jsonl: v_alignbit_b32 / v_add3_u32 streams 4.23,
 # full-rate VOP2 streams 2.13): a loop of A half-rate and B full-rate
 # instructions cannot issue in fewer than A x 4.23 + B x 2.13 SIMD cycles.
-VARIANT_PROFILE = "profiles/r02_variant_report.jsonl"
+VARIANT_PROFILE = "profiles/r02d_variant_report.jsonl"
 IDEAL_COST_A, IDEAL_COST_B = 4.23, 2.13
 
 
@@ -144,8 +144,11 @@ def mix_roofline():
 
 
 def fast_variant(msg_len, d, k=3):
-    """(FV, NV, TRAIL) the planner picks for a d-digit decade of a message of
-    msg_len bytes at lo-digit count k (planner.hpp make_layout/add_fast)."""
+    """(FV, MODE, TRAIL) the planner picks for a d-digit decade of a message
+    of msg_len bytes at lo-digit count k (planner.hpp make_layout/add_fast;
+    MODE as in scan_core.hpp fast_thread: 1 = lo digits in one word, 3/4 =
+    straddling lo digits split with the hundreds / hundreds and tens in the
+    outer word)."""
     r = (msg_len + 1) % 64
     q = r + d - 1
     nb = 1 if r + d + 9 <= 64 else 2
@@ -159,7 +162,9 @@ def fast_variant(msg_len, d, k=3):
         vb, trail, k = 1, False, q - 63
     qv = q - 64 * vb
     fv = (qv - k + 1) >> 2
-    return fv, (qv >> 2) - fv + 1, trail
+    if (qv >> 2) == fv:
+        return fv, 1, trail
+    return fv, 4 if k >= 2 and ((qv - 1) >> 2) == fv else 3, trail
 
 
 def workload_mix(msg_len, lo, hi):

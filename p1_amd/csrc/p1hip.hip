@@ -36,9 +36,9 @@ extern "C" const unsigned char p1hip_kernels_co[];
 
 using namespace p1;
 
-static bool has_variant(int fv, int nv, bool trail) {
-#define P1_CASE(FV, NV, TR) \
-  if (fv == FV && nv == NV && trail == TR) return true;
+static bool has_variant(int fv, int mode, bool trail) {
+#define P1_CASE(FV, MODE, TR) \
+  if (fv == FV && mode == MODE && trail == TR) return true;
 #include "fast_variants.inc"
 #undef P1_CASE
   return false;
@@ -107,7 +107,10 @@ struct Runtime {
   //                           ranges so every k = 3 variant runs on the GPU)
   //   P1HIP_TEST_FAIL_DEVICE  device index whose scan phase reports a failure
   //                           (exercises the multi-device error path)
+  //   P1HIP_NO_SPLIT          straddling lo digits use mode 2 instead of the
+  //                           split modes (A/B builds with -DP1_NV2_PLAIN)
   uint64_t min_fast_threads = kMinFastThreads;
+  bool split = true;
   int fail_device = -1;
   p1hip_stats_t stats{};
 };
@@ -194,6 +197,8 @@ int init_devs(Runtime& R, const std::vector<int>& ords) {
   R.rccl_one = force && force[0] == '1' && R.use_rccl;
   const char* mft = getenv("P1HIP_MIN_FAST_THREADS");
   R.min_fast_threads = mft && *mft ? strtoull(mft, nullptr, 10) : kMinFastThreads;
+  const char* nsp = getenv("P1HIP_NO_SPLIT");
+  R.split = !(nsp && nsp[0] == '1');
   const char* fdev = getenv("P1HIP_TEST_FAIL_DEVICE");
   R.fail_device = fdev && *fdev ? atoi(fdev) : -1;
   if ((nd > 1 || R.rccl_one) && R.use_rccl) {
@@ -223,13 +228,13 @@ int ensure_init(Runtime& R) {
 
 // Run one device's share [lo, hi] (lo <= hi) and leave its Key in d.d_res.
 int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, bool profiling,
-              uint64_t min_fast_threads) {
+              uint64_t min_fast_threads, bool split) {
   HIPCHK(hipSetDevice(d.ordinal));
   d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
   d.scan_launches = d.scan_nonces = d.scan_ops = 0;
   d.fast_ms = d.scan_ms = 0.0;
   Plan plan;
-  std::string err = make_plan(msg, len, lo, hi, plan, true, min_fast_threads);
+  std::string err = make_plan(msg, len, lo, hi, plan, true, min_fast_threads, split);
   if (!err.empty()) return fail(P1HIP_ERR_ARGS, "planner: " + err);
   // Longest-running workgroups first: fast pieces by lo-loop length (10^k),
   // then generic pieces, so short work fills the grid's drain.
@@ -295,8 +300,8 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
       S.block0 = block0;
       block0 += L.blocks;
       if (L.fast) {
-        if (!has_variant(L.fv, L.nv, L.trail)) return fail(P1HIP_ERR_ARGS, "no fast kernel variant");
-        S.kind = variant_id(L.fv, L.nv, L.trail);
+        if (!has_variant(L.fv, L.mode, L.trail)) return fail(P1HIP_ERR_ARGS, "no fast kernel variant");
+        S.kind = variant_id(L.fv, L.mode, L.trail);
         S.fa = L.fa;
         d.fast_launches++;
         d.fast_nonces += L.nonces;
@@ -439,7 +444,7 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
       if ((int)i == R.fail_device) {
         r = fail(P1HIP_ERR_HIP, "injected failure (P1HIP_TEST_FAIL_DEVICE)");
       } else if (active[i]) {
-        r = run_range(d, msg, msg_len, slo[i], shi[i], R.profiling, R.min_fast_threads);
+        r = run_range(d, msg, msg_len, slo[i], shi[i], R.profiling, R.min_fast_threads, R.split);
       } else {
         // empty shard: contribute the identity key (all ones)
         if (hipSetDevice(d.ordinal) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipSetDevice");

@@ -115,7 +115,7 @@ inline void make_tmpl(const Prefix& P, int d, int zero_digits, uint32_t tmpl[32]
 
 struct Launch {
   bool fast;
-  int fv, nv;
+  int fv, nv, mode;  // mode: scan_core.hpp fast_thread
   bool trail;
   FastArgs fa;
   GenArgs ga;
@@ -162,7 +162,11 @@ inline void add_generic(const Prefix& P, const Layout& Y, uint64_t s, uint64_t e
 }
 
 // Returns an empty string on success, else a description of the problem.
-inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint64_t he, Plan& plan) {
+// `split`: lo digits that straddle two words use the split variants (modes
+// 3/4: the first word's work hoisted per 100 or per 10 nonces) rather than
+// updating both words per nonce (mode 2).
+inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint64_t he, Plan& plan,
+                            bool split = true) {
   const int k = Y.k;  // may be below make_layout's choice (see make_plan)
   const int qv = Y.q - 64 * Y.vb;          // last digit inside the variable block
   const int fv = (qv - k + 1) >> 2;
@@ -184,6 +188,12 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
     const int slot = (p >> 2) - fv;
     dlt[t][slot] = 1u << (24 - 8 * (p & 3));
   }
+  // units are always in the last word; mode 3 = only the hundreds digit in
+  // word FV, mode 4 = tens (and hundreds) in word FV
+  int mode = 1;
+  if (nv == 2) mode = !split ? 2 : (k >= 2 && dlt[1][0] != 0) ? 4 : 3;
+  if (mode >= 3 && dlt[0][0] != 0) return "internal: split variant with the units digit in the outer word";
+  if (mode == 3 && dlt[1][0] != 0) return "internal: mode 3 with the tens digit in the outer word";
   FastArgs fa;
   memset(&fa, 0, sizeof fa);
   memcpy(fa.mid, P.mid, sizeof P.mid);
@@ -214,6 +224,7 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
     Ln.fast = true;
     Ln.fv = fv;
     Ln.nv = nv;
+    Ln.mode = mode;
     Ln.trail = Y.trail;
     Ln.fa = fa;
     Ln.fa.hi_first = cur;
@@ -238,7 +249,7 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
 // tests pass 1 so that k = 3 (and the NV = 2, PRE and TRAIL variants it
 // selects) is exercised on ranges the oracle finishes in seconds.
 inline std::string make_plan(const uint8_t* msg, size_t L, uint64_t lower, uint64_t upper, Plan& plan,
-                             bool fast_ok = true, uint64_t min_fast_threads = kMinFastThreads) {
+                             bool fast_ok = true, uint64_t min_fast_threads = kMinFastThreads, bool split = true) {
   Prefix P;
   make_prefix(msg, L, P);
   plan = Plan();
@@ -269,7 +280,7 @@ inline std::string make_plan(const uint8_t* msg, size_t L, uint64_t lower, uint6
       continue;
     }
     if (hs * B > s) add_generic(P, Y, s, hs * B - 1, plan);
-    std::string err = add_fast(P, Y, hs, he, plan);
+    std::string err = add_fast(P, Y, hs, he, plan, split);
     if (!err.empty()) return err;
     if (e % B != B - 1) add_generic(P, Y, (he + 1) * B, e, plan);
   }

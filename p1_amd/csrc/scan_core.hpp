@@ -146,6 +146,18 @@ struct FastPre {
                     //   a = s1.v[0] + W[FV], e = s1.v[4] + W[FV], rest as is
 };
 
+// The invariant half of round T: everything but the "+ W[T]" that the
+// per-nonce word contributes (a = t1 + t2 + W[T], e = d + t1 + W[T]).
+template <int T>
+P1_HD void round_half(const State& s, State& out) {
+  const uint32_t a = s.v[0], b = s.v[1], c = s.v[2], d = s.v[3];
+  const uint32_t e = s.v[4], f = s.v[5], g = s.v[6], h = s.v[7];
+  const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + k256(T);  // + W[T] per nonce
+  const uint32_t t2 = bsig0(a) + maj(a, b, c);
+  out.v[0] = t1 + t2; out.v[1] = a; out.v[2] = b; out.v[3] = c;
+  out.v[4] = d + t1;  out.v[5] = e; out.v[6] = f; out.v[7] = g;
+}
+
 template <int FV, int NV, bool TRAIL>
 P1_HD uint64_t fast_hash(const FastPre<FV, NV, TRAIL>& P, uint32_t wv0, uint32_t wv1, const uint32_t* kw2) {
   using FP = FastPre<FV, NV, TRAIL>;
@@ -183,33 +195,13 @@ P1_HD uint64_t fast_hash(const FastPre<FV, NV, TRAIL>& P, uint32_t wv0, uint32_t
   }
 }
 
+// Per-thread invariants of variant <FV, NV, TRAIL>: P.cv must hold the
+// chaining value entering the variable block; Wt are its 16 message words
+// (hi digits placed, lo digits '0'), wu the uniform word after the per-nonce
+// ones, wlen the bit-length word.
 template <int FV, int NV, bool TRAIL>
-P1_HD Key fast_thread(const FastArgs& A, uint32_t tid) {
+P1_HD void make_pre(FastPre<FV, NV, TRAIL>& P, const uint32_t Wt[16], uint32_t wu, uint32_t wlen) {
   using FP = FastPre<FV, NV, TRAIL>;
-  const bool valid = tid < A.nthreads;
-  const uint64_t hi = A.hi_first + (valid ? tid : 0u);
-
-  uint32_t T[32];
-  place_digits(A.tmpl, hi, A.dh, A.p_last, T);
-
-  FP P;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) P.cv[i] = A.mid[i];
-  const bool pre = A.pre != 0;
-  if (pre) {  // tail block 0 holds only prefix bytes and hi digits
-    uint32_t w[64];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = T[i];
-    compress_full(P.cv, w);
-  }
-  // variable block = tail block `pre`; a mask blend (not a select) keeps the
-  // compiler from lowering this to a runtime-indexed scratch array
-  const uint32_t pm = 0u - (uint32_t)pre;
-  uint32_t Wt[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) Wt[i] = (T[i] & ~pm) | (T[16 + i] & pm);
-  const uint32_t wu = (FV + NV < 16) ? (pre ? A.tmpl[16 + FV + NV] : A.tmpl[FV + NV]) : 0u;
-  const uint32_t wlen = pre ? A.tmpl[31] : A.tmpl[15];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     if (i < FV) P.wI[i] = Wt[i];
@@ -247,40 +239,159 @@ P1_HD Key fast_thread(const FastArgs& A, uint32_t tid) {
   for (int i = 0; i < 8; ++i) s.v[i] = P.cv[i];
 #pragma unroll
   for (int t = 0; t < FV; ++t) sha_round(s, P.kw[t]);
-  {
-    const uint32_t a = s.v[0], b = s.v[1], c = s.v[2], d = s.v[3];
-    const uint32_t e = s.v[4], f = s.v[5], g = s.v[6], h = s.v[7];
-    const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + k256(FV);  // + W[FV] per nonce
-    const uint32_t t2 = bsig0(a) + maj(a, b, c);
-    P.s1.v[0] = t1 + t2; P.s1.v[1] = a; P.s1.v[2] = b; P.s1.v[3] = c;
-    P.s1.v[4] = d + t1;  P.s1.v[5] = e; P.s1.v[6] = f; P.s1.v[7] = g;
-  }
+  round_half<FV>(s, P.s1);
+}
 
-  uint32_t wv0 = Wt[FV];
-  uint32_t wv1 = (NV == 2) ? Wt[FV + 1] : 0u;
+// Split variants (modes 3, 4): the lo digits straddle words O and O+1, but
+// word O changes only every 100 (mode 3: hundreds digit alone in O) or every
+// 10 nonces (mode 4: hundreds and tens in O).  Per thread: the invariants of
+// <O, 2> (nothing depends on W[O] or W[O+1]).  Per change of W[O]: this
+// update to the invariants of <O+1, 1> -- round O, the invariant half of
+// round O+1, and only the schedule terms that come from words depending on
+// W[O] but not on W[O+1].  Per nonce: the <O+1, 1> loop, which hoists one
+// more round and more schedule words than <O, 2>.
+template <int O, bool TRAIL>
+P1_HD void outer_update(const FastPre<O, 2, TRAIL>& B, uint32_t wO, FastPre<O + 1, 1, TRAIL>& P) {
+  using FB = FastPre<O, 2, TRAIL>;
+  using FI = FastPre<O + 1, 1, TRAIL>;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) P.cv[i] = B.cv[i];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) P.wI[i] = (i == O) ? wO : B.wI[i];
+  uint32_t wx[64];  // full values of the words in var(O,2) \ var(O+1,1)
+#pragma unroll
+  for (int t = 0; t < 16; ++t) wx[t] = (t == O) ? wO : 0u;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) P.kw[t] = B.kw[t];
+#pragma unroll
+  for (int t = 16; t < 64; ++t) {
+    if (!FB::var(t)) {
+      P.kw[t] = B.kw[t];  // K + W, untouched by either word
+      wx[t] = 0u;
+      continue;
+    }
+    uint32_t v = B.kw[t];  // terms from words independent of W[O], W[O+1]
+    if (FB::var(t - 2) && !FI::var(t - 2)) v = add2(v, ssig1(wx[t - 2]));
+    if (FB::var(t - 7) && !FI::var(t - 7)) v = add2(v, wx[t - 7]);
+    if (FB::var(t - 15) && !FI::var(t - 15)) v = add2(v, ssig0(wx[t - 15]));
+    if (FB::var(t - 16) && !FI::var(t - 16)) v = add2(v, wx[t - 16]);
+    if (FI::var(t)) {
+      P.kw[t] = v;  // still a partial sum: it also depends on W[O+1]
+      wx[t] = 0u;
+    } else {
+      wx[t] = v;  // complete now
+      P.kw[t] = k256(t) + v;
+    }
+  }
+  // round O with its word, then the invariant half of round O+1
+  State s = B.s1;
+  s.v[0] = add2(s.v[0], wO);
+  s.v[4] = add2(s.v[4], wO);
+  round_half<O + 1>(s, P.s1);
+}
+
+// Thread setup shared by all fast variants: hi digits placed into the tail,
+// PRE block compressed, the variable block's words.
+struct FastSetup {
+  uint64_t hi;
+  bool valid;
+  uint32_t cv[8];
+  uint32_t Wt[16];
+  uint32_t wlen;
+};
+
+P1_HD void fast_setup(const FastArgs& A, uint32_t tid, FastSetup& S) {
+  S.valid = tid < A.nthreads;
+  S.hi = A.hi_first + (S.valid ? tid : 0u);
+  uint32_t T[32];
+  place_digits(A.tmpl, S.hi, A.dh, A.p_last, T);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) S.cv[i] = A.mid[i];
+  const bool pre = A.pre != 0;
+  if (pre) {  // tail block 0 holds only prefix bytes and hi digits
+    uint32_t w[64];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = T[i];
+    compress_full(S.cv, w);
+  }
+  // variable block = tail block `pre`; a mask blend (not a select) keeps the
+  // compiler from lowering this to a runtime-indexed scratch array
+  const uint32_t pm = 0u - (uint32_t)pre;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) S.Wt[i] = (T[i] & ~pm) | (T[16 + i] & pm);
+  S.wlen = pre ? A.tmpl[31] : A.tmpl[15];
+}
+
+P1_HD uint32_t uniform_word(const FastArgs& A, int i) {  // the tail word after the per-nonce ones
+  return i < 16 ? (A.pre ? A.tmpl[16 + i] : A.tmpl[i]) : 0u;
+}
+
+// MODE of a fast variant (how the lo digits sit in the variable block):
+//   1  all in word FV (NV = 1)
+//   2  in words FV and FV+1, both updated per nonce (NV = 2)
+//   3  hundreds in FV, tens and units in FV+1: split, W[FV] work per 100 nonces
+//   4  hundreds and tens in FV, units in FV+1: split, W[FV] work per 10 nonces
+P1_HD constexpr int mode_nv(int mode) { return mode == 1 ? 1 : 2; }
+
+template <int FV, int MODE, bool TRAIL>
+P1_HD Key fast_thread(const FastArgs& A, uint32_t tid) {
+  constexpr int NV = mode_nv(MODE);
+  FastSetup S;
+  fast_setup(A, tid, S);
+  FastPre<FV, NV, TRAIL> P;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) P.cv[i] = S.cv[i];
+  make_pre<FV, NV, TRAIL>(P, S.Wt, uniform_word(A, FV + NV), S.wlen);
+
+  uint32_t wv0 = S.Wt[FV];
+  uint32_t wv1 = (NV == 2) ? S.Wt[FV + 1] : 0u;
   uint64_t best = ~0ull;
   uint32_t bestc = 0;
   uint32_t c = 0;
-  for (uint32_t c2 = 0; c2 < A.n2; ++c2) {
-    for (uint32_t c1 = 0; c1 < A.n1; ++c1) {
-      for (uint32_t c0 = 0; c0 < 10u; ++c0) {
-        const uint64_t h = fast_hash<FV, NV, TRAIL>(P, wv0, wv1, A.kw2);
-        const bool lt = h < best;  // strict '<': first minimum wins (miner.go:59)
-        best = lt ? h : best;
-        bestc = lt ? c : bestc;
-        ++c;
-        wv0 += A.du[0];
-        if (NV == 2) wv1 += A.du[1];
+  if constexpr (MODE <= 2) {
+    for (uint32_t c2 = 0; c2 < A.n2; ++c2) {
+      for (uint32_t c1 = 0; c1 < A.n1; ++c1) {
+        for (uint32_t c0 = 0; c0 < 10u; ++c0) {
+          const uint64_t h = fast_hash<FV, NV, TRAIL>(P, wv0, wv1, A.kw2);
+          const bool lt = h < best;  // strict '<': first minimum wins (miner.go:59)
+          best = lt ? h : best;
+          bestc = lt ? c : bestc;
+          ++c;
+          wv0 += A.du[0];
+          if (NV == 2) wv1 += A.du[1];
+        }
+        wv0 += A.dt[0];
+        if (NV == 2) wv1 += A.dt[1];
       }
-      wv0 += A.dt[0];
-      if (NV == 2) wv1 += A.dt[1];
+      wv0 += A.dhd[0];
+      if (NV == 2) wv1 += A.dhd[1];
     }
-    wv0 += A.dhd[0];
-    if (NV == 2) wv1 += A.dhd[1];
+  } else {
+    // split: W[FV] changes only in the hundreds (MODE 3) or tens (MODE 4)
+    // step (host-checked: du[0] == 0, and dt[0] == 0 for MODE 3)
+    FastPre<FV + 1, 1, TRAIL> Q;
+    for (uint32_t c2 = 0; c2 < A.n2; ++c2) {
+      if (MODE == 3) outer_update<FV, TRAIL>(P, wv0, Q);
+      for (uint32_t c1 = 0; c1 < A.n1; ++c1) {
+        if (MODE == 4) outer_update<FV, TRAIL>(P, wv0, Q);
+        for (uint32_t c0 = 0; c0 < 10u; ++c0) {
+          const uint64_t h = fast_hash<FV + 1, 1, TRAIL>(Q, wv1, 0u, A.kw2);
+          const bool lt = h < best;  // strict '<': first minimum wins (miner.go:59)
+          best = lt ? h : best;
+          bestc = lt ? c : bestc;
+          ++c;
+          wv1 += A.du[1];
+        }
+        if (MODE == 4) wv0 += A.dt[0];
+        wv1 += A.dt[1];
+      }
+      wv0 += A.dhd[0];
+      wv1 += A.dhd[1];
+    }
   }
   Key k;
-  k.h = valid ? best : ~0ull;
-  k.n = valid ? hi * (uint64_t)A.kpow + bestc : ~0ull;
+  k.h = S.valid ? best : ~0ull;
+  k.n = S.valid ? S.hi * (uint64_t)A.kpow + bestc : ~0ull;
   return k;
 }
 

@@ -15,12 +15,27 @@ U64_MAX = (1 << 64) - 1
 EMU = os.path.join(ROOT, "tools", "p1emu")
 
 
-def emu(msg, lo, hi, generic=False, minthreads=None):
+def emu(msg, lo, hi, generic=False, minthreads=None, nosplit=False, variants=None):
     args = [EMU, msg.hex() if msg else "-", str(lo), str(hi)] + (["generic"] if generic else [])
     if minthreads is not None:
         args.append(f"minthreads={minthreads}")
+    if nosplit:
+        args.append("nosplit")
     out = subprocess.run(args, capture_output=True, text=True, check=True).stdout.split()
+    if variants is not None and out[4] != "-":
+        variants.update(tuple(int(x) for x in v.split(":")) for v in out[4].split(","))
     return (int(out[0]), int(out[1])), int(out[2]), int(out[3])
+
+
+def all_variants(plain_mode2):
+    """(FV, MODE, TRAIL) of every P1_CASE in fast_variants.inc; the mode-2
+    block is compiled only with -DP1_NV2_PLAIN (p1emu is)."""
+    with open(os.path.join(ROOT, "p1_amd", "csrc", "fast_variants.inc")) as f:
+        text = f.read()
+    if not plain_mode2:
+        text = text.split("#ifdef P1_NV2_PLAIN")[0]
+    return {(int(a), int(b), 1 if c == "true" else 0)
+            for a, b, c in re.findall(r"P1_CASE\((\d+), (\d+), (true|false)\)", text)}
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -64,20 +79,27 @@ def test_emu_every_layout(oracle_mod):
             assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
 
 
-def test_emu_every_layout_k3(oracle_mod):
+@pytest.mark.parametrize("nosplit", [False, True], ids=["split", "plain2"])
+def test_emu_every_layout_k3(oracle_mod, nosplit):
     """Planner occupancy floor at 1 thread: k = 3 on small ranges, so every
-    (FV, NV, TRAIL) variant, PRE/TRAIL at k = 3 and the tens/hundreds carry
-    deltas (dt/dhd) are replayed against the oracle."""
+    (FV, MODE, TRAIL) variant, PRE/TRAIL at k = 3 and the tens/hundreds carry
+    deltas (dt/dhd) are replayed against the oracle.  The
+    default pass runs the split modes 3/4 for straddling lo digits (what the
+    library ships); the plain2 pass runs mode 2 (both words per nonce).  Both
+    must reach every variant they can select."""
     rnd = random.Random(8)
+    seen = set()
     for L in range(0, 128):
         m = bytes(rnd.randrange(32, 127) for _ in range(L))
         for d in (5, 9, 10, 11, 12, 20):
             b = 10 ** (d - 1)
             lo = b + rnd.randrange(0, 10**4) if d < 20 else b
             hi = min(lo + 4999, U64_MAX)
-            got, nf, _ = emu(m, lo, hi, minthreads=1)
+            got, nf, _ = emu(m, lo, hi, minthreads=1, nosplit=nosplit, variants=seen)
             assert nf >= 1
             assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
+    want = {v for v in all_variants(True) if (v[1] == 2) == nosplit or v[1] == 1}
+    assert seen == want, sorted(want ^ seen)
 
 
 def test_emu_range_top(oracle_mod):

@@ -7,10 +7,13 @@
 // CPU-only test suite.  It is never part of libp1hip.so and never used to
 // produce a product result.
 //
-// usage: p1emu <msg-hex> <lower> <upper> [generic | minthreads=N]
+// usage: p1emu <msg-hex> <lower> <upper> [generic | minthreads=N] [nosplit]
 //   minthreads=N sets the planner's occupancy floor (1 keeps k = 3 on small
-//   ranges, so every k = 3 variant is replayed)
-//   prints "<hash> <nonce> <fast_launches> <generic_launches>"
+//   ranges, so every k = 3 variant is replayed); nosplit uses mode 2 for
+//   straddling lo digits (p1emu is built with -DP1_NV2_PLAIN)
+//   prints "<hash> <nonce> <fast_launches> <generic_launches> <variants>"
+//   where <variants> lists the fast variants run as FV:MODE:TRAIL,... ("-"
+//   when none)
 #include <inttypes.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -23,22 +26,22 @@
 
 using namespace p1;
 
-template <int FV, int NV, bool TR>
+template <int FV, int MODE, bool TR>
 static Key run_fast(const FastArgs& A, uint64_t threads) {
   Key best = {~0ull, ~0ull};
   for (uint64_t t = 0; t < threads; ++t) {
-    Key k = fast_thread<FV, NV, TR>(A, (uint32_t)t);
+    Key k = fast_thread<FV, MODE, TR>(A, (uint32_t)t);
     if (key_lt(k, best)) best = k;
   }
   return best;
 }
 
 static Key dispatch_fast(const Launch& L) {
-#define P1_CASE(FV, NV, TR) \
-  if (L.fv == FV && L.nv == NV && L.trail == TR) return run_fast<FV, NV, TR>(L.fa, L.threads);
+#define P1_CASE(FV, MODE, TR) \
+  if (L.fv == FV && L.mode == MODE && L.trail == TR) return run_fast<FV, MODE, TR>(L.fa, L.threads);
 #include "../p1_amd/csrc/fast_variants.inc"
 #undef P1_CASE
-  fprintf(stderr, "no fast variant fv=%d nv=%d trail=%d\n", L.fv, L.nv, (int)L.trail);
+  fprintf(stderr, "no fast variant fv=%d mode=%d trail=%d\n", L.fv, L.mode, (int)L.trail);
   exit(3);
 }
 
@@ -63,12 +66,17 @@ int main(int argc, char** argv) {
   const uint64_t upper = strtoull(argv[3], nullptr, 10);
   const bool generic_only = argc > 4 && strcmp(argv[4], "generic") == 0;
   uint64_t min_threads = kMinFastThreads;
-  if (argc > 4 && strncmp(argv[4], "minthreads=", 11) == 0) min_threads = strtoull(argv[4] + 11, nullptr, 10);
+  bool split = true;
+  for (int i = 4; i < argc; ++i) {
+    if (strncmp(argv[i], "minthreads=", 11) == 0) min_threads = strtoull(argv[i] + 11, nullptr, 10);
+    if (strcmp(argv[i], "nosplit") == 0) split = false;
+  }
   Key best = {~0ull, ~0ull};
   int nf = 0, ng = 0;
+  std::string vars;
   if (lower <= upper) {
     Plan plan;
-    std::string err = make_plan(msg.data(), msg.size(), lower, upper, plan, !generic_only, min_threads);
+    std::string err = make_plan(msg.data(), msg.size(), lower, upper, plan, !generic_only, min_threads, split);
     if (!err.empty()) {
       fprintf(stderr, "plan error: %s\n", err.c_str());
       return 1;
@@ -78,6 +86,9 @@ int main(int argc, char** argv) {
       if (L.fast) {
         ++nf;
         k = dispatch_fast(L);
+        char v[32];
+        snprintf(v, sizeof v, "%s%d:%d:%d", vars.empty() ? "" : ",", L.fv, L.mode, (int)L.trail);
+        vars += v;
       } else {
         ++ng;
         k = {~0ull, ~0ull};
@@ -90,6 +101,6 @@ int main(int argc, char** argv) {
     }
   }
   if (best.h == ~0ull) best.n = 0;  // identity of miner.go:56
-  printf("%" PRIu64 " %" PRIu64 " %d %d\n", best.h, best.n, nf, ng);
+  printf("%" PRIu64 " %" PRIu64 " %d %d %s\n", best.h, best.n, nf, ng, vars.empty() ? "-" : vars.c_str());
   return 0;
 }

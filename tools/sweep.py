@@ -8,7 +8,7 @@ HIP-event time (library profiling, as bench.py does) and from the host wall
 time of p1hip_scan.  The reported nonce must re-hash to the reported hash
 (oracle).  Prints one JSON line per case and a summary line.
 
-Per case: the fast variant (FV, NV, TRAIL) the planner picks, the algorithmic
+Per case: the fast variant (FV, MODE, TRAIL) the planner picks, the algorithmic
 roofline fraction (1384 x B_tail ops per nonce at the kernel rate over
 78.64 TOP/s, the bench.py accounting).
 """
@@ -22,27 +22,14 @@ sys.path.insert(0, ROOT)
 
 import oracle  # noqa: E402  (checker only)
 import p1_amd  # noqa: E402
+from bench import fast_variant  # noqa: E402
 
 PEAK = 256 * 4 * 32 * 2.4e9
 
 
-def variant(L, d, k=3):
-    """(FV, NV, TRAIL) of the fast path for message length L, d digits
-    (planner.hpp make_layout / add_fast with the default k)."""
-    r = (L + 1) % 64
-    q = r + d - 1
-    nb = 1 if r + d + 9 <= 64 else 2
-    if nb == 1:
-        vb, trail = 0, False
-    elif q <= 63:
-        vb, trail = 0, True
-    elif q - 64 >= 2:
-        vb, trail = 1, False
-    else:
-        vb, trail, k = 1, False, q - 63
-    qv = q - 64 * vb
-    fv = (qv - k + 1) >> 2
-    return fv, (qv >> 2) - fv + 1, trail
+def variant(L, d):
+    """(FV, MODE, TRAIL) of the fast path for message length L, d digits."""
+    return fast_variant(L, d)
 
 
 def main():
