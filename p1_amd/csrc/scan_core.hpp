@@ -164,22 +164,38 @@ P1_HD uint64_t fast_hash(const FastPre<FV, NV, TRAIL>& P, uint32_t wv0, uint32_t
   uint32_t w[64];
 #pragma unroll
   for (int i = 0; i < 16; ++i) w[i] = (i == FV) ? wv0 : (NV == 2 && i == FV + 1) ? wv1 : P.wI[i];
+  // P1_SCHED_JIT (A/B builds only): form each variant schedule word right
+  // before its round instead of all of them first.  It keeps the live set to
+  // the 16-word window -- the c2 loop then fits 64 VGPRs without spills, for
+  // an 8-wave build -- but costs FV <= 1 loops ~14% more instructions and
+  // gains nothing at 8 waves ("Occupancy budget").
+  constexpr bool kJit =
+#ifdef P1_SCHED_JIT
+      true;
+#else
+      false;
+#endif
+  auto sched_var = [&](int t) {
+    uint32_t v = P.kw[t];
+    if (FP::var(t - 2)) v = add2(v, ssig1(w[t - 2]));
+    if (FP::var(t - 7)) v = add2(v, w[t - 7]);
+    if (FP::var(t - 15)) v = add2(v, ssig0(w[t - 15]));
+    if (FP::var(t - 16)) v = add2(v, w[t - 16]);
+    w[t] = v;
+  };
+  if constexpr (!kJit) {
 #pragma unroll
-  for (int t = 16; t < 64; ++t) {
-    if (FP::var(t)) {
-      uint32_t v = P.kw[t];
-      if (FP::var(t - 2)) v = add2(v, ssig1(w[t - 2]));
-      if (FP::var(t - 7)) v = add2(v, w[t - 7]);
-      if (FP::var(t - 15)) v = add2(v, ssig0(w[t - 15]));
-      if (FP::var(t - 16)) v = add2(v, w[t - 16]);
-      w[t] = v;
-    }
+    for (int t = 16; t < 64; ++t)
+      if (FP::var(t)) sched_var(t);
   }
   State s = P.s1;
   s.v[0] = add2(s.v[0], wv0);  // round FV, per-nonce half
   s.v[4] = add2(s.v[4], wv0);
 #pragma unroll
-  for (int t = FV + 1; t < 64; ++t) sha_round(s, FP::var(t) ? k256(t) + w[t] : P.kw[t]);
+  for (int t = FV + 1; t < 64; ++t) {
+    if (kJit && t >= 16 && FP::var(t)) sched_var(t);
+    sha_round(s, FP::var(t) ? k256(t) + w[t] : P.kw[t]);
+  }
   if constexpr (!TRAIL) {
     return ((uint64_t)(P.cv[0] + s.v[0]) << 32) | (uint64_t)(P.cv[1] + s.v[1]);
   } else {
