@@ -85,19 +85,20 @@ class UsageError(SystemExit):
     pass
 
 
-def resolve_run(gpus, config, env, visible):
+def resolve_run(gpus, config, env, visible, force_dist=False):
     """How this invocation uses the GPUs.
 
     Returns a dict: mode ("single" | "library" | "torchrun"), n (GPUs in the
     job), rank, world (processes), local_rank, config.  Raises UsageError
     (non-zero exit) when the request cannot be honoured -- never falls back to
-    fewer GPUs than asked for."""
+    fewer GPUs than asked for.  force_dist (--dist) takes the torchrun path
+    even for a world of one process, to rehearse it on a one-GPU box."""
     world = int(env.get("WORLD_SIZE", "1") or 1)
     rank = int(env.get("RANK", "0") or 0)
     local = int(env.get("LOCAL_RANK", "0") or 0)
     if gpus < 1:
         raise UsageError(f"bench.py: --gpus must be >= 1 (got {gpus})")
-    if world > 1:
+    if world > 1 or force_dist:
         if gpus != world:
             raise UsageError(f"bench.py: --gpus {gpus} but torchrun started {world} ranks (WORLD_SIZE)")
         mode, n = "torchrun", world
@@ -276,6 +277,9 @@ def main():
     ap.add_argument("--no-small-request", action="store_true",
                     help="skip the configs[0]-sized latency probe (profiling runs: keeps every "
                          "k_scan launch in the rocprof summary a workload launch)")
+    ap.add_argument("--dist", action="store_true",
+                    help="take the one-process-per-GPU torch.distributed path even when WORLD_SIZE is 1 "
+                         "(rehearses the driver's N>1 launch, RCCL included, on one GPU)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torchrun path: nccl = RCCL over xGMI (production); gloo only to rehearse "
                          "several ranks on one GPU")
@@ -286,7 +290,7 @@ def main():
     visible = torch.cuda.device_count()
     try:
         run = resolve_run(args.gpus, args.config, os.environ,
-                          visible if args.dist_backend == "nccl" else max(visible, args.gpus))
+                          visible if args.dist_backend == "nccl" else max(visible, args.gpus), args.dist)
     except UsageError as e:
         print(str(e), file=sys.stderr)
         sys.exit(2)
@@ -303,6 +307,7 @@ def main():
 
     msg = cfg["msg"]
     total = job_total(cfg, n_gpus)
+    t_init = time.perf_counter()  # device init, module load, communicators: reported, not timed
     if mode == "torchrun":
         gpu = run["local_rank"] % visible if args.dist_backend == "gloo" else run["local_rank"]
         torch.cuda.set_device(gpu)
@@ -321,6 +326,7 @@ def main():
             sys.exit(2)
         devices = list(range(n_gpus))
         sync_devs = devices
+    init_ms = (time.perf_counter() - t_init) * 1e3
 
     def step():
         if mode == "torchrun":
@@ -339,9 +345,13 @@ def main():
     p1_amd.set_profiling(True)
     barrier()
     t0 = time.perf_counter()
-    results = [step() for _ in range(args.steps)]
+    results, marks = [], [t0]
+    for _ in range(args.steps):
+        results.append(step())  # synchronous: the (hash, nonce) result is on the host
+        marks.append(time.perf_counter())
     barrier()
     elapsed = time.perf_counter() - t0
+    step_ms = sorted((b - a) * 1e3 for a, b in zip(marks, marks[1:]))
     p1_amd.set_profiling(False)
     stats = p1_amd.get_stats()
 
@@ -432,6 +442,12 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
+            # SURVEY.md 8(d) timing: per-step wall times (first enqueue to the
+            # host min) of this rank, median of the K steps; one-time setup
+            # (devices, code object, communicators) is outside the timed region
+            "step_ms": {"median": statistics.median(step_ms), "min": step_ms[0], "max": step_ms[-1],
+                        "n": len(step_ms), "rank": rank} if step_ms else None,
+            "init_ms": init_ms,
             "higher_is_better": True,
             "scaling": "strong" if "total" in cfg else "weak",
             "vs_baseline": value * 1e9 / PUBLISHED_HASHES_PER_S,

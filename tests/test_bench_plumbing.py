@@ -72,3 +72,10 @@ def test_cli_refuses_more_gpus_than_visible():
 def test_host_cores_reports_model():
     n, aff, quota, model = bench.host_cores()
     assert 1 <= n <= aff and model
+
+
+def test_dist_flag_rehearses_torchrun_path_at_world_one():
+    # torchrun --nproc-per-node 1 bench.py --gpus 1 --dist: the RCCL path on one GPU
+    r = bench.resolve_run(1, "c4", {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, visible=1, force_dist=True)
+    assert r["mode"] == "torchrun" and r["n"] == 1 and r["world"] == 1
+    assert bench.resolve_run(1, None, {}, visible=1)["mode"] == "single"  # the driver's N=1 launch

@@ -32,6 +32,11 @@ if [ "${RUN_TORCHRUN:-0}" = 1 ]; then
   # rehearse the N>1 launch path on one GPU: 2 ranks, gloo all-gather, shared device
   step torchrun2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 "$ROOT/bench.py" --gpus 2 --steps 2 --warmup 1 --dist-backend gloo > "$OUT/${TAG}_torchrun2.json" 2> "$OUT/${TAG}_torchrun2.err"
 fi
+if [ "${RUN_DIST1:-0}" = 1 ]; then
+  # the driver's N>1 code path (torch.distributed "nccl" = RCCL, device_id,
+  # all-gather of the 16-B partials, all-reduce of the step time) at world 1
+  step dist1_nccl 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29512 "$ROOT/bench.py" --gpus 1 --dist --config c4 --steps 2 --warmup 1 --no-cpu > "$OUT/${TAG}_dist1_nccl.json" 2> "$OUT/${TAG}_dist1_nccl.err"
+fi
 for lib in ${VARIANTS:-}; do
   n=$(basename "$lib" .so)
   P1HIP_LIB="$ROOT/$lib" step "bench_$n" 600 python "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu > "$OUT/${TAG}_bench_$n.json" 2> "$OUT/${TAG}_bench_$n.err"
