@@ -4,7 +4,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall
 LLVM ?= /opt/rocm/lib/llvm/bin
 CSRC := p1_amd/csrc
-HDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/planner.hpp $(CSRC)/fast_variants.inc \
+HDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/planner.hpp $(CSRC)/fast_variants.inc $(CSRC)/variant_cost.inc \
         $(CSRC)/scan_abi.hpp include/p1hip.h
 # device code: HIP C++ -> gfx950 assembly -> tools/isa_post.py peephole
 # (VOP2 -> VOP3 encodings of full-rate integer ops, every inner loop started

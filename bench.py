@@ -330,7 +330,7 @@ def main():
 
     def step():
         if mode == "torchrun":
-            return distributed_scan(msg, 0, total - 1, p1_amd.scan, device=coll_dev)
+            return distributed_scan(msg, 0, total - 1, p1_amd.scan, device=coll_dev, shard_fn=p1_amd.plan_shards)
         return p1_amd.scan(msg, 0, total - 1)  # library: shards + RCCL all-gather inside
 
     def barrier():
@@ -429,9 +429,10 @@ def main():
             mix["frac"] = k_rate / 1e9 / mix["peak_GH_s"]
             roofline["mix_roofline"] = mix
         parallelism = {"single": "1 GPU",
-                       "library": f"range-shard x{n_gpus}, one process (p1hip_init({n_gpus}): thread per device, "
+                       "library": f"cost-balanced contiguous range-shard x{n_gpus} (p1hip_plan_shards), one process (p1hip_init({n_gpus}): thread per device, "
                                   f"ncclCommInitAll + ncclAllGather of 16-B partials)",
-                       "torchrun": f"range-shard x{n_gpus}, one process per GPU + "
+                       "torchrun": f"cost-balanced contiguous range-shard x{n_gpus} (p1hip_plan_shards), "
+                                   "one process per GPU + "
                                    + ("RCCL all-gather (torch.distributed nccl)" if args.dist_backend == "nccl"
                                       else "gloo all-gather (rehearsal)")}[mode]
         line = {

@@ -62,11 +62,25 @@ int p1hip_init_devices(const int *ordinals, int n);
  * in the range equals UINT64_MAX the nonce is 0 (identity of miner.go:56).
  * Documented divergence: upper == UINT64_MAX is scanned inclusively and the
  * call returns; the Go loop wraps (i++) and never terminates.
- * With several devices the range is split contiguously across them and the
- * 16-byte per-device partials are combined by an RCCL all-gather + host min.
+ * With several devices the range is split contiguously across them
+ * (p1hip_plan_shards) and the 16-byte per-device partials are combined by an
+ * RCCL all-gather + host min.
  * Lazily calls p1hip_init(0, NULL) if nothing is initialised. */
 int p1hip_scan(const uint8_t *msg, size_t msg_len, uint64_t lower, uint64_t upper,
                uint64_t *out_hash, uint64_t *out_nonce);
+
+/* The contiguous split p1hip_scan uses across devices, for callers that
+ * shard themselves (one process per GPU, or a server handing miners pieces
+ * of one request, server.go:119-140): [lower, upper] (inclusive) into n >= 1
+ * shards of near-equal predicted GPU time, in order; shard i is
+ * [first[i], last[i]], and first[i] > last[i] marks an empty shard.  Host
+ * only (no device needed).  Kernel variants differ in cost per nonce by
+ * decade (digit count), so equal-count shards over different decades would
+ * finish at different times.  Contiguous shards keep the lexicographic min
+ * of the shard results equal to the serial first-minimum of miner.go:56-63.
+ * lower > upper gives n empty shards. */
+int p1hip_plan_shards(const uint8_t *msg, size_t msg_len, uint64_t lower, uint64_t upper, int n,
+                      uint64_t *first, uint64_t *last);
 
 /* bitcoin.Hash(msg, nonce) (hash.go:13-17), computed on the GPU as the
  * one-nonce scan [nonce, nonce]. */

@@ -16,6 +16,7 @@ from ._lib import (  # noqa: F401
     scan,
     hash,
     reduce_pairs,
+    plan_shards,
     set_profiling,
     get_stats,
     reset_stats,

@@ -51,6 +51,8 @@ SIGNATURES = [
     ("p1hip_scan", ctypes.c_int,
      [ctypes.c_char_p, ctypes.c_size_t, U64, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
     ("p1hip_hash", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, U64, ctypes.POINTER(U64)]),
+    ("p1hip_plan_shards", ctypes.c_int,
+     [ctypes.c_char_p, ctypes.c_size_t, U64, U64, ctypes.c_int, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
     ("p1hip_reduce_pairs", ctypes.c_int,
      [ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.c_size_t, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
     ("p1hip_set_profiling", ctypes.c_int, [ctypes.c_int]),
@@ -116,6 +118,16 @@ def hash(msg, nonce):  # noqa: A001 - mirrors bitcoin.Hash
     h = U64()
     _check(load().p1hip_hash(m, len(m), int(nonce), ctypes.byref(h)))
     return h.value
+
+
+def plan_shards(msg, lower, upper, n):
+    """p1hip_plan_shards: [lower, upper] cut into n contiguous shards of
+    near-equal predicted GPU time; a list of inclusive (lo, hi) or None for
+    an empty shard.  Host-only: needs the library, not a device."""
+    m = _bytes(msg)
+    first, last = (U64 * n)(), (U64 * n)()
+    _check(load().p1hip_plan_shards(m, len(m), int(lower), int(upper), int(n), first, last))
+    return [(a, b) if a <= b else None for a, b in zip(first, last)]
 
 
 def reduce_pairs(hashes, nonces):

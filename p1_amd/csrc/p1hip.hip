@@ -71,7 +71,20 @@ int fail(int rc, const std::string& what) {
   } while (0)
 
 constexpr uint32_t kMaxSegs = 64;              // segments per launch
-constexpr uint32_t kMaxLaunchBlocks = 1u << 20;  // workgroups per launch
+// Workgroups per launch: 2^22 x 256 threads stays below HIP's 2^32-thread
+// grid limit and keeps configs[3] on one GPU (2^38 nonces, ~1.07M
+// workgroups) in one launch, i.e. one grid drain per scan.
+constexpr uint32_t kMaxLaunchBlocks = 1u << 22;
+
+// P1HIP_MAX_LAUNCH_BLOCKS (tests only, read per scan): a lower per-launch
+// workgroup cap, so a full-size GPU test still runs the multi-launch path.
+// Never below one fast piece (kMaxFastThreads / kBlock workgroups).
+uint64_t launch_block_limit() {
+  const char* v = getenv("P1HIP_MAX_LAUNCH_BLOCKS");
+  const uint64_t n = v && *v ? strtoull(v, nullptr, 10) : 0;
+  if (n == 0 || n >= kMaxLaunchBlocks) return kMaxLaunchBlocks;
+  return n < kMaxFastThreads / kBlock ? kMaxFastThreads / kBlock : n;
+}
 
 struct Dev {
   int ordinal = -1;
@@ -107,6 +120,8 @@ struct Runtime {
   //                           ranges so every k = 3 variant runs on the GPU)
   //   P1HIP_TEST_FAIL_DEVICE  device index whose scan phase reports a failure
   //                           (exercises the multi-device error path)
+  //   P1HIP_MAX_LAUNCH_BLOCKS workgroups per k_scan launch (read per scan,
+  //                           launch_block_limit)
   //   P1HIP_NO_SPLIT          straddling lo digits use mode 2 instead of the
   //                           split modes (A/B builds with -DP1_NV2_PLAIN)
   uint64_t min_fast_threads = kMinFastThreads;
@@ -254,13 +269,14 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
   std::vector<Batch> batches;
   uint64_t all_blocks = 0;
   for (const Launch& L : plan.launches) all_blocks += L.blocks;
-  const uint64_t nlaunch = (all_blocks + kMaxLaunchBlocks - 1) / kMaxLaunchBlocks;
-  const uint64_t target = nlaunch > 1 ? (all_blocks + nlaunch - 1) / nlaunch : kMaxLaunchBlocks;
+  const uint64_t max_blocks = launch_block_limit();
+  const uint64_t nlaunch = (all_blocks + max_blocks - 1) / max_blocks;
+  const uint64_t target = nlaunch > 1 ? (all_blocks + nlaunch - 1) / nlaunch : max_blocks;
   uint32_t total_blocks = 0;
   for (size_t r = 0; r < order.size(); ++r) {
     const Launch& L = plan.launches[order[r]];
     const uint64_t cur = batches.empty() ? 0 : batches.back().blocks;
-    if (batches.empty() || batches.back().count == kMaxSegs || cur + (uint64_t)L.blocks > kMaxLaunchBlocks ||
+    if (batches.empty() || batches.back().count == kMaxSegs || cur + (uint64_t)L.blocks > max_blocks ||
         (cur > 0 && cur + L.blocks / 2 > target && batches.size() < nlaunch))  // fits the next batch better
       batches.push_back({r, 0, 0});
     batches.back().count++;
@@ -401,23 +417,11 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
   Key res = {~0ull, 0};
   if (lower <= upper) {
     const size_t nd = R.devs.size();
-    // contiguous shards: shard i = [lo_i, hi_i]
-    const uint64_t span = upper - lower;  // count - 1
+    // contiguous shards of near-equal predicted cost (planner.hpp plan_shards)
     std::vector<uint64_t> slo(nd), shi(nd);
     std::vector<char> active(nd, 0);
-    {
-      const uint64_t per = span / nd, extra = span % nd;
-      uint64_t cur = lower;
-      for (size_t i = 0; i < nd; ++i) {
-        // sizes: per (+1 for the first `extra`), +1 on the last -> sum span+1
-        uint64_t cnt = per + (i < extra ? 1u : 0u) + (i + 1 == nd ? 1u : 0u);
-        if (cnt == 0) continue;
-        active[i] = 1;
-        slo[i] = cur;
-        shi[i] = cur + (cnt - 1);
-        cur += cnt;
-      }
-    }
+    plan_shards(msg, msg_len, lower, upper, (int)nd, slo.data(), shi.data());
+    for (size_t i = 0; i < nd; ++i) active[i] = slo[i] <= shi[i];
     // Phase 1: every device scans its shard and synchronises its stream.
     // Phase 2 (the collective) starts only when every device succeeded, so a
     // failing device can never leave its peers blocked inside ncclAllGather.
@@ -506,6 +510,19 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out_hash = res.h;
   *out_nonce = res.n;
+  return P1HIP_OK;
+}
+
+int p1hip_plan_shards(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t upper, int n,
+                      uint64_t* first, uint64_t* last) {
+  if (n <= 0 || !first || !last) return fail(P1HIP_ERR_ARGS, "n <= 0 or null output");
+  if (!msg && msg_len > 0) return fail(P1HIP_ERR_ARGS, "msg == NULL with msg_len > 0");
+  if (msg_len > P1HIP_MAX_MSG_LEN) return fail(P1HIP_ERR_ARGS, "msg_len exceeds P1HIP_MAX_MSG_LEN");
+  if (lower > upper) {
+    for (int i = 0; i < n; ++i) { first[i] = 1; last[i] = 0; }
+    return P1HIP_OK;
+  }
+  plan_shards(msg, msg_len, lower, upper, n, first, last);
   return P1HIP_OK;
 }
 

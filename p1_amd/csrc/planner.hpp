@@ -161,6 +161,25 @@ inline void add_generic(const Prefix& P, const Layout& Y, uint64_t s, uint64_t e
   }
 }
 
+// The fast variant <FV, MODE, TRAIL> that runs layout Y at Y.k lo digits:
+// FV = first tail word of the variable block holding a lo digit, NV = words
+// holding lo digits (1 or 2).  Units are always in the last word; with two
+// words, mode 3 = only the hundreds digit in word FV, mode 4 = the tens (and
+// hundreds) there, mode 2 = both words updated per nonce (split = false).
+struct Variant {
+  int fv, nv, mode;
+};
+
+inline Variant fast_variant(const Layout& Y, bool split = true) {
+  const int qv = Y.q - 64 * Y.vb;
+  Variant v;
+  v.fv = (qv - Y.k + 1) >> 2;
+  v.nv = (qv >> 2) - v.fv + 1;
+  v.mode = 1;
+  if (v.nv == 2) v.mode = !split ? 2 : (Y.k >= 2 && ((qv - 1) >> 2) == v.fv) ? 4 : 3;
+  return v;
+}
+
 // Returns an empty string on success, else a description of the problem.
 // `split`: lo digits that straddle two words use the split variants (modes
 // 3/4: the first word's work hoisted per 100 or per 10 nonces) rather than
@@ -169,9 +188,8 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
                             bool split = true) {
   const int k = Y.k;  // may be below make_layout's choice (see make_plan)
   const int qv = Y.q - 64 * Y.vb;          // last digit inside the variable block
-  const int fv = (qv - k + 1) >> 2;
-  const int jl = qv >> 2;
-  const int nv = jl - fv + 1;
+  const Variant var = fast_variant(Y, split);
+  const int fv = var.fv, nv = var.nv;
   uint32_t tmpl[32];
   int nb = 0;
   make_tmpl(P, Y.d, k, tmpl, &nb);
@@ -190,10 +208,10 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
   }
   // units are always in the last word; mode 3 = only the hundreds digit in
   // word FV, mode 4 = tens (and hundreds) in word FV
-  int mode = 1;
-  if (nv == 2) mode = !split ? 2 : (k >= 2 && dlt[1][0] != 0) ? 4 : 3;
+  const int mode = var.mode;
   if (mode >= 3 && dlt[0][0] != 0) return "internal: split variant with the units digit in the outer word";
   if (mode == 3 && dlt[1][0] != 0) return "internal: mode 3 with the tens digit in the outer word";
+  if (mode == 4 && dlt[1][0] == 0) return "internal: mode 4 without the tens digit in the outer word";
   FastArgs fa;
   memset(&fa, 0, sizeof fa);
   memcpy(fa.mid, P.mid, sizeof P.mid);
@@ -285,6 +303,115 @@ inline std::string make_plan(const uint8_t* msg, size_t L, uint64_t lower, uint6
     if (e % B != B - 1) add_generic(P, Y, (he + 1) * B, e, plan);
   }
   return std::string();
+}
+
+// ---------------------------------------------------------------------------
+// Cost-balanced contiguous shards (multi-device scans, one shard per device
+// or rank).  Every nonce of a decade runs the same kernel variant, and the
+// variants differ by up to 2x in cost (TRAIL layouts hash two blocks; a
+// variant's cost falls as FV grows).  Equal-count shards therefore finish at
+// different times when they cover different decades (configs[3] on 8 GPUs:
+// the d = 11 shards run `4,1`, 2% slower per nonce than d = 12's `4,4`), and
+// a multi-GPU scan waits for its slowest shard.  plan_shards cuts [lower,
+// upper] where the predicted cost, not the nonce count, reaches i/n of the
+// total.  The cut points are still contiguous, so the lexicographic min of
+// the shard results is the serial first-minimum (miner.go:56-63).
+// ---------------------------------------------------------------------------
+
+// SIMD cycles per wave-instruction of the two issue classes at 4 waves/SIMD
+// with 8-byte instructions at 4 mod 8 (tools/valu_runs).
+constexpr double kCyclesA = 4.37, kCyclesB = 2.66;
+// A nonce with nothing hoisted (generic kernel; also the per-thread prologue
+// of a fast thread): ~1384 ops per block plus the digit formatting.
+constexpr double kUnhoistedCyclesPerBlock = 1600.0 * 3.6;
+
+// Predicted SIMD cycles per wave of 64 nonces of variant <fv, mode, trail>'s
+// loop (variant_cost.inc: VALU counts of each variant's per-nonce loop, read
+// from the shipped code object by tools/variant_report.py); 0 if not listed.
+inline double variant_cycles(int fv, int mode, bool trail) {
+#define P1_COST(FV, MODE, TR, A, B) \
+  if (fv == FV && mode == MODE && trail == TR) return (A) * kCyclesA + (B) * kCyclesB;
+#include "variant_cost.inc"
+#undef P1_COST
+  return 0.0;
+}
+
+// Predicted cost of one nonce of decade d (d digits) for a message whose
+// prefix is P: the fast variant's loop plus its per-thread prologue spread
+// over the 10^k nonces of a thread, or the generic kernel for d <= k.
+inline double nonce_cycles(const Prefix& P, int d) {
+  const Layout Y = make_layout(P.r, d);
+  const double unhoisted = kUnhoistedCyclesPerBlock * Y.nb;
+  if (d <= Y.k) return unhoisted;
+  const Variant v = fast_variant(Y);
+  double c = variant_cycles(v.fv, v.mode, Y.trail);
+  if (c <= 0.0) c = 1384.0 * 3.6 * Y.nb;
+  return c + unhoisted / (double)pow10u(Y.k);
+}
+
+// Split [lower, upper] (inclusive, lower <= upper) into n >= 1 contiguous
+// shards of near-equal predicted cost: shard i = [first[i], last[i]], in
+// order; first[i] > last[i] marks an empty shard (fewer nonces than shards).
+// `cost[i]`, if not null, receives each shard's predicted cost (SIMD cycles
+// per 64 nonces, summed).
+inline void plan_shards(const uint8_t* msg, size_t L, uint64_t lower, uint64_t upper, int n, uint64_t* first,
+                        uint64_t* last, double* cost = nullptr) {
+  typedef unsigned __int128 u128;
+  Prefix P;
+  make_prefix(msg, L, P);
+  struct Piece { uint64_t s, e; double c; };
+  std::vector<Piece> pcs;
+  double total = 0.0;
+  for (int d = 1; d <= 20; ++d) {
+    const uint64_t dlo = (d == 1) ? 0u : pow10u(d - 1);
+    const uint64_t dhi = (d == 20) ? ~0ull : pow10u(d) - 1u;
+    const uint64_t s = lower > dlo ? lower : dlo;
+    const uint64_t e = upper < dhi ? upper : dhi;
+    if (s > e) continue;
+    const Piece pc = {s, e, nonce_cycles(P, d)};
+    pcs.push_back(pc);
+    total += ((double)(e - s) + 1.0) * pc.c;
+  }
+  std::vector<u128> cut((size_t)n + 1);
+  cut[0] = lower;
+  cut[n] = (u128)upper + 1u;
+  size_t j = 0;
+  double before = 0.0;  // cost of pieces [0, j)
+  for (int i = 1; i < n; ++i) {
+    const double t = total * (double)i / (double)n;
+    while (j < pcs.size() && before + ((double)(pcs[j].e - pcs[j].s) + 1.0) * pcs[j].c <= t) {
+      before += ((double)(pcs[j].e - pcs[j].s) + 1.0) * pcs[j].c;
+      ++j;
+    }
+    u128 x = cut[n];
+    if (j < pcs.size()) {
+      const double off = (t - before) / pcs[j].c;
+      const uint64_t span = pcs[j].e - pcs[j].s;
+      const uint64_t o = off <= 0.0 ? 0u : off >= (double)span ? span : (uint64_t)off;
+      x = (u128)pcs[j].s + o;
+    }
+    if (x < cut[i - 1]) x = cut[i - 1];
+    if (x > cut[n]) x = cut[n];
+    cut[i] = x;
+  }
+  for (int i = 0; i < n; ++i) {
+    if (cut[i] < cut[i + 1]) {
+      first[i] = (uint64_t)cut[i];
+      last[i] = (uint64_t)(cut[i + 1] - 1u);
+    } else {
+      first[i] = 1;
+      last[i] = 0;
+    }
+    if (cost) {
+      cost[i] = 0.0;
+      if (first[i] > last[i]) continue;
+      for (const Piece& pc : pcs) {
+        const uint64_t s = pc.s > first[i] ? pc.s : first[i];
+        const uint64_t e = pc.e < last[i] ? pc.e : last[i];
+        if (s <= e) cost[i] += ((double)(e - s) + 1.0) * pc.c;
+      }
+    }
+  }
 }
 
 }  // namespace p1

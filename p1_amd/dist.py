@@ -19,13 +19,21 @@ def _to_u64(v):
     return v + (1 << 64) if v < 0 else v
 
 
-def distributed_scan(msg, lower, upper, scan_fn, device=None, group=None):
+def distributed_scan(msg, lower, upper, scan_fn, device=None, group=None, shard_fn=None):
     """Scan [lower, upper] with every rank of `group` taking one contiguous
     shard through scan_fn(msg, lo, hi) -> (hash, nonce); returns the global
-    result on every rank."""
+    result on every rank.
+
+    shard_fn(msg, lower, upper, world) -> [(lo, hi) | None] * world picks the
+    shards (default: equal nonce counts, sharding.shard_range); the GPU path
+    passes p1_amd.plan_shards, the library's cost-balanced contiguous split.
+    Every rank must use the same shard_fn."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
-    s = shard_range(lower, upper, rank, world)
+    if shard_fn is None:
+        s = shard_range(lower, upper, rank, world)
+    else:
+        s = shard_fn(msg, lower, upper, world)[rank]
     key = scan_fn(msg, s[0], s[1]) if s is not None else (2**64 - 1, 0)
     t = torch.tensor([_to_i64(key[0]), _to_i64(key[1])], dtype=torch.int64, device=device)
     out = torch.empty(2 * world, dtype=torch.int64, device=device)

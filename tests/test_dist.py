@@ -16,7 +16,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, cases, q):
+def _worker(rank, world, port, cases, q, planned=False):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -34,19 +34,25 @@ def _worker(rank, world, port, cases, q):
         calls.append((lo, hi))
         return oracle.scan(m, lo, hi)
 
-    out = [distributed_scan(m, lo, hi, scan_fn) for m, lo, hi in cases]
+    shard_fn = None
+    if planned:
+        import p1_amd
+
+        shard_fn = p1_amd.plan_shards  # host-only library call: no device needed
+    out = [distributed_scan(m, lo, hi, scan_fn, shard_fn=shard_fn) for m, lo, hi in cases]
     dist.destroy_process_group()
     q.put((rank, out, calls))
 
 
+@pytest.mark.parametrize("planned", [False, True], ids=["equal", "plan_shards"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_distributed_scan_gloo(world, oracle_mod):
+def test_distributed_scan_gloo(world, planned, oracle_mod):
     cases = [(b"bradfitz", 0, 9999), (b"msg", 0, 2), (b"x" * 70, 10**9 - 2000, 10**9 + 2000),
              (b"bradfitz", 5, 3), (b"msg", 0, 0)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, planned)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -57,7 +63,8 @@ def test_distributed_scan_gloo(world, oracle_mod):
     for rank, out, calls in res:
         assert out == want, rank
         # every rank scanned exactly its own contiguous shard
-        from p1_amd import shard_range
+        from p1_amd import plan_shards, shard_range
 
-        exp = [shard_range(lo, hi, rank, world) for _, lo, hi in cases]
+        exp = [plan_shards(m, lo, hi, world)[rank] if planned else shard_range(lo, hi, rank, world)
+               for m, lo, hi in cases]
         assert calls == [e for e in exp if e is not None]

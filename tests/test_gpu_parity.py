@@ -188,14 +188,22 @@ def test_reduce_pairs_large(gpu):
     assert gpu.reduce_pairs(hs, ns) == want
 
 
-def test_config4_range_on_one_gpu_multi_batch(gpu, oracle_mod):
-    """configs[3]'s whole [0, 2^38) on one GPU: > 2^20 workgroups, so the scan
-    is split into several launches (batches).  Checked by size-independent
-    properties: re-hash of the result and min of two halves (single batch
-    each)."""
+def test_config4_range_on_one_gpu_multi_batch(gpu, oracle_mod, monkeypatch):
+    """configs[3]'s whole [0, 2^38) on one GPU (~1.07M workgroups): one
+    launch by default, and several launches (batches) under a 2^19-workgroup
+    cap (test knob P1HIP_MAX_LAUNCH_BLOCKS, read per scan).  Checked by
+    size-independent properties: both agree, the result re-hashes on the
+    oracle and equals the min of two independently scanned halves."""
     hi = (1 << 38) - 1
+    gpu.reset_stats()
     h, n = gpu.scan("bradfitz", 0, hi)
+    assert gpu.get_stats()["scan_launches"] == 1
     assert oracle_mod.hash("bradfitz", n) == h
+    monkeypatch.setenv("P1HIP_MAX_LAUNCH_BLOCKS", str(1 << 19))
+    gpu.reset_stats()
+    assert gpu.scan("bradfitz", 0, hi) == (h, n)
+    assert gpu.get_stats()["scan_launches"] >= 2
+    monkeypatch.delenv("P1HIP_MAX_LAUNCH_BLOCKS")
     a = gpu.scan("bradfitz", 0, (1 << 37) - 1)
     b = gpu.scan("bradfitz", 1 << 37, hi)
     assert min(a, b) == (h, n)

@@ -102,6 +102,65 @@ def test_emu_every_layout_k3(oracle_mod, nosplit):
     assert seen == want, sorted(want ^ seen)
 
 
+def _variant_cost_table():
+    with open(os.path.join(ROOT, "p1_amd", "csrc", "fast_variants.inc")) as f:
+        shipped = {(int(a), int(b), c == "true")
+                   for a, b, c in re.findall(r"P1_CASE\((\d+), (\d+), (true|false)\)", f.read().split("#ifdef")[0])}
+    with open(os.path.join(ROOT, "p1_amd", "csrc", "variant_cost.inc")) as f:
+        table = {(int(a), int(b), c == "true"): (int(x), int(y))
+                 for a, b, c, x, y in re.findall(r"P1_COST\((\d+), (\d+), (true|false), (\d+), (\d+)\)", f.read())}
+    return shipped, table
+
+
+def test_variant_cost_table_covers_shipped_variants():
+    """plan_shards prices every variant the library can run."""
+    shipped, table = _variant_cost_table()
+    assert shipped <= set(table), sorted(shipped - set(table))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 9])
+def test_plan_shards_contiguous_cover(n):
+    """p1hip_plan_shards (host only): shards in order, contiguous, exactly
+    [lower, upper]; empty shards only when there are fewer nonces than
+    shards; lower > upper gives all-empty."""
+    import p1_amd
+
+    rnd = random.Random(n)
+    cases = [(b"bradfitz", 0, 2**38 - 1), (b"cmu440-p1-" * 12, 0, 2**34 - 1), (b"", 0, U64_MAX),
+             (b"msg", U64_MAX - 5, U64_MAX), (b"msg", 0, 0), (b"msg", 3, 5), (b"x" * 63, 99, 10**12 + 7)]
+    cases += [(bytes(rnd.randrange(256) for _ in range(rnd.randrange(200))),) +
+              tuple(sorted((rnd.randrange(2**64), rnd.randrange(2**64)))) for _ in range(20)]
+    for msg, lo, hi in cases:
+        shards = p1_amd.plan_shards(msg, lo, hi, n)
+        assert len(shards) == n
+        got = [s for s in shards if s is not None]
+        assert got[0][0] == lo and got[-1][1] == hi
+        for (a, b), (c, _) in zip(got, got[1:]):
+            assert a <= b and c == b + 1
+        if hi - lo + 1 >= n:
+            assert len(got) == n
+    assert p1_amd.plan_shards(b"msg", 7, 6, 3) == [None, None, None]
+
+
+def test_plan_shards_cost_balance():
+    """configs[3] over 8 shards: the d = 11 decade runs variant <4,1>, d = 12
+    runs <4,4> (fewer loop instructions per nonce), so the planned shards
+    inside d = 11 hold fewer nonces than those inside d = 12, in the ratio of
+    the variants' predicted loop cycles (A 4.37 + B 2.66 per instruction)."""
+    import p1_amd
+
+    _, table = _variant_cost_table()
+    cyc = {v: a * 4.37 + b * 2.66 for v, (a, b) in table.items()}
+    shards = p1_amd.plan_shards(b"bradfitz", 0, 2**38 - 1, 8)
+    size = [b - a + 1 for a, b in shards]
+    assert sum(size) == 2**38
+    assert 10**10 <= shards[1][0] and shards[1][1] < 10**11      # all d = 11
+    assert 10**11 <= shards[5][0]                                 # all d = 12
+    want = cyc[(4, 4, False)] / cyc[(4, 1, False)]
+    assert abs(size[1] / size[5] - want) < 2e-3
+    assert size[1] < 2**35 < size[5]
+
+
 def test_emu_range_top(oracle_mod):
     for m in (b"msg", b"x" * 60):
         got, _, _ = emu(m, U64_MAX - 2500, U64_MAX)
