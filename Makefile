@@ -6,6 +6,8 @@ LLVM ?= /opt/rocm/lib/llvm/bin
 CSRC := p1_amd/csrc
 HDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/planner.hpp $(CSRC)/fast_variants.inc $(CSRC)/variant_cost.inc \
         $(CSRC)/scan_abi.hpp include/p1hip.h
+# what the device code includes (the host-side planner does not rebuild it)
+DEVHDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/fast_variants.inc $(CSRC)/scan_abi.hpp
 # device code: HIP C++ -> gfx950 assembly -> tools/isa_post.py peephole
 # (VOP2 -> VOP3 encodings of full-rate integer ops, every inner loop started
 # at 4 mod 8 bytes; see DESIGN.md "Build") -> assembled + linked code object,
@@ -17,7 +19,7 @@ BUILD := build
 all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios \
      tools/lsp_fake_miner
 
-$(BUILD)/p1hip_kernels.s: $(CSRC)/p1hip_kernels.hip $(HDRS)
+$(BUILD)/p1hip_kernels.s: $(CSRC)/p1hip_kernels.hip $(DEVHDRS)
 	mkdir -p $(BUILD)
 	$(HIPCC) $(DEVFLAGS) -S -o $@ $(CSRC)/p1hip_kernels.hip
 
