@@ -94,7 +94,10 @@ int p1hip_reduce_pairs(const uint64_t *hashes, const uint64_t *nonces, size_t n,
                        uint64_t *out_hash, uint64_t *out_nonce);
 
 /* Kernel-level accounting.  One p1hip_scan = one (rarely several) launch of
- * the scan kernel k_scan per device, covering every decade of the range. */
+ * the scan kernel k_scan per device, covering every decade of the range; a
+ * share of at most 2^16 nonces is one launch of k_scan_small instead (plan in
+ * the kernel arguments, reduce fused into the last workgroup, result written
+ * to pinned host memory). */
 typedef struct {
   uint64_t scans;            /* p1hip_scan calls since reset                      */
   uint64_t fast_launches;    /* fast segments (one thread per 10^k nonces)        */
@@ -109,6 +112,8 @@ typedef struct {
   uint64_t scan_alg_ops;     /* their algorithmic int32 ops (1384 * B_tail each)  */
   double scan_kernel_ms;     /* sum of HIP-event durations of those launches
                                 (recorded only while profiling is on)            */
+  uint64_t small_scans;      /* device scans that took the one-launch small path
+                                (<= 2^16 nonces: k_scan_small, fused reduce)     */
 } p1hip_stats_t;
 
 /* Record HIP events (on the library's own stream) around every fast-kernel

@@ -32,6 +32,7 @@ class Stats(ctypes.Structure):
         ("scan_nonces", U64),
         ("scan_alg_ops", U64),
         ("scan_kernel_ms", ctypes.c_double),
+        ("small_scans", U64),
     ]
 
     def as_dict(self):

@@ -76,6 +76,16 @@ constexpr uint32_t kMaxSegs = 64;              // segments per launch
 // workgroups) in one launch, i.e. one grid drain per scan.
 constexpr uint32_t kMaxLaunchBlocks = 1u << 22;
 
+// P1HIP_SMALL_MAX_NONCES (tests only, read per scan): ranges of at most this
+// many nonces take the one-launch small path (default kSmallMaxNonces; 0
+// turns it off so small parity ranges exercise the fast kernel variants).
+uint64_t small_limit() {
+  const char* v = getenv("P1HIP_SMALL_MAX_NONCES");
+  if (!v || !*v) return kSmallMaxNonces;
+  const uint64_t n = strtoull(v, nullptr, 10);
+  return n < kSmallMaxNonces ? n : kSmallMaxNonces;
+}
+
 // P1HIP_MAX_LAUNCH_BLOCKS (tests only, read per scan): a lower per-launch
 // workgroup cap, so a full-size GPU test still runs the multi-launch path.
 // Never below one fast piece (kMaxFastThreads / kBlock workgroups).
@@ -99,7 +109,10 @@ struct Dev {
   size_t seg_cap = 0;           // launch slots allocated
   ncclComm_t comm = nullptr;
   hipModule_t mod = nullptr;    // embedded code object, loaded on this device
-  hipFunction_t f_scan = nullptr, f_reduce = nullptr, f_pairs = nullptr;
+  hipFunction_t f_scan = nullptr, f_reduce = nullptr, f_pairs = nullptr, f_small = nullptr;
+  Key* d_small_part = nullptr;  // kSmallMaxBlocks partials of k_scan_small
+  uint32_t* d_ticket = nullptr; // k_scan_small's last-workgroup counter (0 between scans)
+  bool small_used = false;      // this scan ran k_scan_small (result already in h_res[0])
   std::vector<hipEvent_t> evs;  // profiling event pool (pairs)
   // per-scan accounting filled by run_range
   uint64_t fast_launches = 0, fast_nonces = 0, fast_ops = 0, gen_launches = 0, gen_nonces = 0;
@@ -147,6 +160,8 @@ int dev_release(Dev& d) {
   if (d.d_part) (void)hipFree(d.d_part);
   if (d.d_res) (void)hipFree(d.d_res);
   if (d.d_gather) (void)hipFree(d.d_gather);
+  if (d.d_small_part) (void)hipFree(d.d_small_part);
+  if (d.d_ticket) (void)hipFree(d.d_ticket);
   if (d.h_res) (void)hipHostFree(d.h_res);
   if (d.stream) (void)hipStreamDestroy(d.stream);
   if (d.mod) (void)hipModuleUnload(d.mod);
@@ -199,6 +214,13 @@ int init_devs(Runtime& R, const std::vector<int>& ords) {
     HIPCHK(hipModuleGetFunction(&d.f_scan, d.mod, "k_scan"));
     HIPCHK(hipModuleGetFunction(&d.f_reduce, d.mod, "k_reduce"));
     HIPCHK(hipModuleGetFunction(&d.f_pairs, d.mod, "k_pairs"));
+    HIPCHK(hipModuleGetFunction(&d.f_small, d.mod, "k_scan_small"));
+    HIPCHK(hipMalloc(&d.d_small_part, sizeof(Key) * kSmallMaxBlocks));
+    HIPCHK(hipMalloc(&d.d_ticket, sizeof(uint32_t)));
+    // on the library's own stream: a null-stream call would give every
+    // process a second hardware queue (8 miner processes share one GPU)
+    HIPCHK(hipMemsetAsync(d.d_ticket, 0, sizeof(uint32_t), d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
     HIPCHK(hipMalloc(&d.d_res, sizeof(Key)));
     HIPCHK(hipMalloc(&d.d_gather, sizeof(Key) * nd));
     HIPCHK(hipHostMalloc(&d.h_res, sizeof(Key) * nd, hipHostMallocDefault));
@@ -239,6 +261,57 @@ int ensure_init(Runtime& R) {
   std::vector<int> ords;
   for (int i = 0; i < count; ++i) ords.push_back(i);
   return init_locked(R, ords);
+}
+
+// Small share [lo, hi] (at most kSmallMaxNonces nonces): one k_scan_small
+// launch; the Key lands in d.d_res and, when `to_host`, in d.h_res[0].
+int run_small(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, bool to_host, bool profiling) {
+  HIPCHK(hipSetDevice(d.ordinal));
+  d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
+  d.scan_launches = d.scan_nonces = d.scan_ops = 0;
+  d.fast_ms = d.scan_ms = 0.0;
+  Plan plan;
+  std::string err = make_plan(msg, len, lo, hi, plan, false);
+  if (!err.empty()) return fail(P1HIP_ERR_ARGS, "planner: " + err);
+  if (plan.launches.size() > kSmallMaxSegs || plan.total_blocks > kSmallMaxBlocks)
+    return fail(P1HIP_ERR_ARGS, "internal: small plan exceeds its argument block");
+  SmallArgs a;
+  memset(&a, 0, sizeof a);
+  uint32_t block0 = 0;
+  for (size_t i = 0; i < plan.launches.size(); ++i) {
+    const Launch& L = plan.launches[i];
+    a.ga[i] = L.ga;
+    a.block0[i] = block0;
+    block0 += L.blocks;
+    d.gen_launches++;
+    d.gen_nonces += L.nonces;
+    d.scan_ops += L.nonces * kAlgOpsPerCompression * (uint64_t)L.btail;
+  }
+  a.nseg = (uint32_t)plan.launches.size();
+  a.nblocks = block0;
+  a.part = d.d_small_part;
+  a.ticket = d.d_ticket;
+  a.out_dev = d.d_res;
+  a.out_host = to_host ? d.h_res : nullptr;
+  if (profiling) {
+    while (d.evs.size() < 2) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      d.evs.push_back(e);
+    }
+    HIPCHK(hipEventRecord(d.evs[0], d.stream));
+  }
+  HIPCHK(launch(d.f_small, a.nblocks, kBlock, d.stream, a));
+  if (profiling) {
+    float ms = 0.f;
+    HIPCHK(hipEventRecord(d.evs[1], d.stream));
+    HIPCHK(hipEventSynchronize(d.evs[1]));
+    HIPCHK(hipEventElapsedTime(&ms, d.evs[0], d.evs[1]));
+    d.scan_ms = ms;
+  }
+  d.scan_launches = 1;
+  d.scan_nonces = plan.total_nonces;
+  return P1HIP_OK;
 }
 
 // Run one device's share [lo, hi] (lo <= hi) and leave its Key in d.d_res.
@@ -442,11 +515,21 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
       return P1HIP_OK;
     };
     const bool coll = (nd > 1 || R.rccl_one) && R.use_rccl;
+    const uint64_t small_max = small_limit();
     run_threads([&](size_t i) {
       Dev& d = R.devs[i];
       int r = P1HIP_OK;
+      // per-scan accounting starts empty on every device (an inactive shard
+      // must not re-report its previous scan)
+      d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
+      d.scan_launches = d.scan_nonces = d.scan_ops = 0;
+      d.fast_ms = d.scan_ms = 0.0;
+      d.small_used = false;
       if ((int)i == R.fail_device) {
         r = fail(P1HIP_ERR_HIP, "injected failure (P1HIP_TEST_FAIL_DEVICE)");
+      } else if (active[i] && shi[i] - slo[i] < small_max) {
+        d.small_used = true;
+        r = run_small(d, msg, msg_len, slo[i], shi[i], !coll && nd == 1, R.profiling);
       } else if (active[i]) {
         r = run_range(d, msg, msg_len, slo[i], shi[i], R.profiling, R.min_fast_threads, R.split);
       } else {
@@ -458,7 +541,7 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
       if (!r && !coll && nd > 1) {  // host combine (P1HIP_NO_RCCL, tests)
         if (hipMemcpyAsync(R.devs[0].h_res + i, d.d_res, sizeof(Key), hipMemcpyDeviceToHost, d.stream) != hipSuccess)
           r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(result)");
-      } else if (!r && !coll) {
+      } else if (!r && !coll && !(active[i] && d.small_used)) {  // the small kernel wrote h_res itself
         if (hipMemcpyAsync(d.h_res, d.d_res, sizeof(Key), hipMemcpyDeviceToHost, d.stream) != hipSuccess)
           r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(result)");
       }
@@ -503,6 +586,7 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
       R.stats.scan_nonces += d.scan_nonces;
       R.stats.scan_alg_ops += d.scan_ops;
       R.stats.scan_kernel_ms += d.scan_ms;
+      if (d.small_used && d.scan_launches) R.stats.small_scans++;
     }
   }
   R.stats.scans++;
@@ -596,7 +680,7 @@ void p1hip_reset_stats(void) {
 
 const char* p1hip_last_error(void) { return g_err.c_str(); }
 
-const char* p1hip_version(void) { return "p1hip 0.2 gfx950"; }
+const char* p1hip_version(void) { return "p1hip 0.3 gfx950"; }
 
 void p1hip_shutdown(void) {
   Runtime& R = rt();

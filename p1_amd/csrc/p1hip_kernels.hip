@@ -130,6 +130,41 @@ extern "C" __global__ __launch_bounds__(kReduceThreads) void k_reduce(const Key*
   block_min_store<kReduceThreads>(b, out);
 }
 
+// Small scans: one launch, whole plan in the kernel arguments (generic pieces,
+// one nonce per thread), the last workgroup to finish folds every partial.
+// Partials cross XCDs (each XCD has its own L2), so the writers release at
+// agent scope before taking a ticket and the last workgroup acquires after.
+extern "C" __global__ __launch_bounds__(kBlock) void k_scan_small(SmallArgs a) {
+  const uint32_t b = blockIdx.x;
+  uint32_t si = 0;
+  while (si + 1 < a.nseg && a.block0[si + 1] <= b) ++si;
+  const Key k = generic_thread(a.ga[si], (uint64_t)(b - a.block0[si]) * kBlock + threadIdx.x);
+  block_min_store<kBlock>(k, a.part + b);
+  __shared__ uint32_t last;
+  if (threadIdx.x == 0) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == a.nblocks - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  Key m = {~0ull, ~0ull};
+  for (uint32_t i = threadIdx.x; i < a.nblocks; i += kBlock) {
+    Key p;
+    p.h = __hip_atomic_load(&a.part[i].h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    p.n = __hip_atomic_load(&a.part[i].n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    m = key_min(m, p);
+  }
+  block_min_store<kBlock>(m, a.out_dev);
+  if (threadIdx.x == 0) {
+    *a.ticket = 0;  // ready for the next scan (launches on the stream are ordered)
+    if (a.out_host) {
+      *a.out_host = *a.out_dev;
+      __atomic_thread_fence(__ATOMIC_RELEASE);  // system-visible before the kernel ends
+    }
+  }
+}
+
 // test hook: one crafted pair per thread -> per-workgroup partials
 extern "C" __global__ __launch_bounds__(kBlock) void k_pairs(const uint64_t* __restrict__ hs,
                                                              const uint64_t* __restrict__ ns, uint64_t n,

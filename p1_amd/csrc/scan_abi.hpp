@@ -26,8 +26,29 @@ struct Segment {
 
 constexpr int kReduceThreads = 1024;  // k_reduce: one workgroup
 
+// Small scans (configs[0]-sized requests, single nonces of p1hip_hash): one
+// launch of k_scan_small with the whole plan in its kernel arguments (no
+// table copy), generic pieces only, and the grid's last workgroup folding the
+// partials (no k_reduce launch) and writing the result straight to pinned
+// host memory (no copy back).  [lower, upper] with at most kSmallMaxNonces
+// nonces spans at most 5 decades, so at most kSmallMaxSegs pieces.
+constexpr uint32_t kSmallMaxSegs = 6;
+constexpr uint64_t kSmallMaxNonces = 1u << 16;
+constexpr uint32_t kSmallMaxBlocks = (uint32_t)(kSmallMaxNonces / kBlock) + kSmallMaxSegs;
+struct SmallArgs {
+  GenArgs ga[kSmallMaxSegs];
+  uint32_t block0[kSmallMaxSegs];  // first workgroup of each piece
+  uint32_t nseg;
+  uint32_t nblocks;                // workgroups in the grid
+  Key* part;                       // kSmallMaxBlocks partials (device)
+  uint32_t* ticket;                // device counter, 0 between scans
+  Key* out_dev;                    // result (device, for the multi-device combine)
+  Key* out_host;                   // result (pinned host) or null
+};
+
 // Kernel entry points (extern "C" names in the code object):
 //   k_scan(const Segment* segs, uint32_t nseg, Key* part)            grid: sum of segment blocks x kBlock
 //   k_reduce(const Key* part, uint32_t n, Key* out)                  grid: 1 x kReduceThreads
 //   k_pairs(const uint64_t* hs, const uint64_t* ns, uint64_t n, Key* part)  grid: ceil(n/kBlock) x kBlock
+//   k_scan_small(SmallArgs a)                                        grid: a.nblocks x kBlock
 }  // namespace p1

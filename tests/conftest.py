@@ -37,6 +37,11 @@ def gpu():
     library or the device is missing: on the GPU box that is a real failure."""
     import p1_amd
 
+    # Shares of <= 2^16 nonces take the one-launch small path (k_scan_small,
+    # generic kernel) in production.  The parity suite's small ranges are
+    # there to exercise the fast kernel variants, so the session turns the
+    # small path off (read per scan); tests/test_gpu_small.py turns it back on.
+    os.environ["P1HIP_SMALL_MAX_NONCES"] = "0"
     p1_amd.load()
     p1_amd.init_devices([0])
     return p1_amd
