@@ -56,7 +56,7 @@ for cfg in ${PROF_CONFIGS:-c2}; do
                "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_IFETCH" \
                "FETCH_SIZE" "WRITE_SIZE"; do
       i=$((i+1))
-      step pmc_${cfg}_$i 300 rocprofv3 --pmc $set --kernel-include-regex '^k_scan' -d "$OUT/${TAG}_${cfg}_pmc$i" -o pmc --output-format csv -- python3 "$ROOT/bench.py" $pargs
+      step pmc_${cfg}_$i 300 rocprofv3 --pmc $set --kernel-include-regex '^k_scan$' -d "$OUT/${TAG}_${cfg}_pmc$i" -o pmc --output-format csv -- python3 "$ROOT/bench.py" $pargs
     done
   fi
 done

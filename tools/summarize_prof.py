@@ -26,7 +26,7 @@ def workload_stats(trace, out):
     """rocprofv3 --kernel-trace rows of the workload's k_scan launches only
     (largest grid; bench.py's configs[0]-sized latency probe launches small
     grids of the same kernel), in the --stats CSV layout."""
-    rows = [r for r in csv.DictReader(open(trace)) if r["Kernel_Name"].startswith("k_scan")]
+    rows = [r for r in csv.DictReader(open(trace)) if r["Kernel_Name"].split("(")[0] == "k_scan"]
     if not rows:
         return
     g = max(int(r["Grid_Size_X"]) for r in rows)
@@ -70,7 +70,7 @@ def main():
         shutil.copy(f, os.path.join(dst, os.path.basename(f)))
     counters, durs, sums = {}, [], {}
     for f in sorted(glob.glob(os.path.join(src, f"{tag}_pmc*", "*counter_collection.csv"))):
-        rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("k_scan")]
+        rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].split("(")[0] == "k_scan"]
         if not rows:
             continue
         # only the workload's own launches (largest grid); bench.py also times
