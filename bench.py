@@ -149,7 +149,7 @@ def fast_variant(msg_len, d, k=3):
     of msg_len bytes at lo-digit count k (planner.hpp make_layout/add_fast;
     MODE as in scan_core.hpp fast_thread: 1 = lo digits in one word, 3/4 =
     straddling lo digits split with the hundreds / hundreds and tens in the
-    outer word)."""
+    outer word, 5 = tail block 1 holds only lo digits, its schedule tabulated)."""
     r = (msg_len + 1) % 64
     q = r + d - 1
     nb = 1 if r + d + 9 <= 64 else 2
@@ -157,10 +157,10 @@ def fast_variant(msg_len, d, k=3):
         vb, trail = 0, False
     elif q <= 63:
         vb, trail = 0, True
-    elif q - 64 >= 2:
-        vb, trail = 1, False
+    elif q - 63 <= 4:
+        return 0, 5, False  # MODE 5: tail block 1 holds only the lo digits (k = q - 63)
     else:
-        vb, trail, k = 1, False, q - 63
+        vb, trail = 1, False
     qv = q - 64 * vb
     fv = (qv - k + 1) >> 2
     if (qv >> 2) == fv:

@@ -114,6 +114,14 @@ struct Dev {
   uint32_t* d_ticket = nullptr; // k_scan_small's last-workgroup counter (0 between scans)
   bool small_used = false;      // this scan ran k_scan_small (result already in h_res[0])
   std::vector<hipEvent_t> evs;  // profiling event pool (pairs)
+  // MODE 5 K+W tables on this device, most recent last (planner.hpp
+  // build_kwtable; keyed by the block-1 template and k)
+  struct KwTab {
+    uint32_t w[16];
+    int k;
+    uint32_t* dptr;
+  };
+  std::vector<KwTab> kwtabs;
   // per-scan accounting filled by run_range
   uint64_t fast_launches = 0, fast_nonces = 0, fast_ops = 0, gen_launches = 0, gen_nonces = 0;
   double fast_ms = 0.0;
@@ -154,6 +162,8 @@ int dev_release(Dev& d) {
   if (d.stream) (void)hipStreamSynchronize(d.stream);
   for (hipEvent_t e : d.evs) (void)hipEventDestroy(e);
   d.evs.clear();
+  for (Dev::KwTab& t : d.kwtabs) (void)hipFree(t.dptr);
+  d.kwtabs.clear();
   if (d.d_seg) (void)hipFree(d.d_seg);
   if (d.h_seg) (void)hipHostFree(d.h_seg);
   if (d.comm) ncclCommDestroy(d.comm);
@@ -314,6 +324,32 @@ int run_small(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
   return P1HIP_OK;
 }
 
+// Device copy of a MODE 5 launch's K+W table (cached: the same layout in
+// later scans reuses it; scans are synchronous, so an evicted table is idle).
+constexpr size_t kMaxKwTabs = 8;
+int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
+  for (Dev::KwTab& t : d.kwtabs)
+    if (t.k == L.Y.k && memcmp(t.w, L.tabw, sizeof t.w) == 0) {
+      *dptr = (uint64_t)(uintptr_t)t.dptr;
+      return P1HIP_OK;
+    }
+  if (d.kwtabs.size() == kMaxKwTabs) {
+    HIPCHK(hipFree(d.kwtabs.front().dptr));
+    d.kwtabs.erase(d.kwtabs.begin());
+  }
+  const std::vector<uint32_t> tab = build_kwtable(L);
+  Dev::KwTab t;
+  memcpy(t.w, L.tabw, sizeof t.w);
+  t.k = L.Y.k;
+  t.dptr = nullptr;
+  HIPCHK(hipMalloc(&t.dptr, tab.size() * sizeof(uint32_t)));
+  d.kwtabs.push_back(t);
+  HIPCHK(hipMemcpyAsync(t.dptr, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
+  HIPCHK(hipStreamSynchronize(d.stream));  // `tab` is freed on return
+  *dptr = (uint64_t)(uintptr_t)t.dptr;
+  return P1HIP_OK;
+}
+
 // Run one device's share [lo, hi] (lo <= hi) and leave its Key in d.d_res.
 int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, bool profiling,
               uint64_t min_fast_threads, bool split) {
@@ -392,6 +428,10 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
         if (!has_variant(L.fv, L.mode, L.trail)) return fail(P1HIP_ERR_ARGS, "no fast kernel variant");
         S.kind = variant_id(L.fv, L.mode, L.trail);
         S.fa = L.fa;
+        if (L.mode == 5) {
+          const int rt = kwtable_for(d, L, &S.fa.kwtab);
+          if (rt != P1HIP_OK) return rt;
+        }
         d.fast_launches++;
         d.fast_nonces += L.nonces;
         d.fast_ops += L.nonces * kAlgOpsPerCompression * (uint64_t)L.btail;

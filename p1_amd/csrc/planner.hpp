@@ -15,8 +15,9 @@
 //      (one thread per nonce).
 //   3. the pieces become the segments of one multi-segment k_scan launch
 //      (p1hip.hip), longest-running workgroups first.
-// k is 3 except where the last 3 digits would straddle the two tail blocks;
-// then k = 1 or 2 so that all lo digits sit in the last block.
+// k is 3, except when the digits reach 1..4 bytes into the second tail block:
+// then k = that count, so that the block holds only lo digits (MODE 5, its
+// message schedule tabulated per lo value) and never a digit of block 0.
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -91,8 +92,8 @@ inline Layout make_layout(uint32_t r, int d) {
   Y.nb = ((int)r + d + 9 <= 64) ? 1 : 2;
   if (Y.nb == 1) { Y.vb = 0; Y.k = 3; Y.trail = false; }
   else if (Y.q <= 63) { Y.vb = 0; Y.k = 3; Y.trail = true; }     // lo digits in block 0
-  else if (Y.q - 64 >= 2) { Y.vb = 1; Y.k = 3; Y.trail = false; } // lo digits in block 1
-  else { Y.vb = 1; Y.k = Y.q - 63; Y.trail = false; }             // q in {64,65}: k = 1, 2
+  else if (Y.q - 63 <= 4) { Y.vb = 1; Y.k = Y.q - 63; Y.trail = false; } // every block-1 digit lo: MODE 5
+  else { Y.vb = 1; Y.k = 3; Y.trail = false; }                          // lo digits in block 1
   return Y;
 }
 
@@ -123,6 +124,11 @@ struct Launch {
   uint32_t blocks;
   uint64_t nonces;
   int btail;
+  Layout Y;           // fast: the layout it was planned with (Y.k = its k)
+  // MODE 5: what its K+W table is built from (build_kwtable); fa.kwtab is
+  // filled in by whoever runs the plan (a device copy in p1hip.hip, a host
+  // copy in tools/p1emu)
+  uint32_t tabw[16];  // tail block 1 words, '0' at the lo digit bytes
 };
 
 struct Plan {
@@ -173,6 +179,12 @@ struct Variant {
 inline Variant fast_variant(const Layout& Y, bool split = true) {
   const int qv = Y.q - 64 * Y.vb;
   Variant v;
+  if (Y.vb == 1 && Y.q - 63 == Y.k) {  // tail block 1 holds only lo digits (in W[0]) and constants
+    v.fv = 0;
+    v.nv = 1;
+    v.mode = 5;
+    return v;
+  }
   v.fv = (qv - Y.k + 1) >> 2;
   v.nv = (qv >> 2) - v.fv + 1;
   v.mode = 1;
@@ -209,7 +221,8 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
   // units are always in the last word; mode 3 = only the hundreds digit in
   // word FV, mode 4 = tens (and hundreds) in word FV
   const int mode = var.mode;
-  if (mode >= 3 && dlt[0][0] != 0) return "internal: split variant with the units digit in the outer word";
+  if ((mode == 3 || mode == 4) && dlt[0][0] != 0)
+    return "internal: split variant with the units digit in the outer word";
   if (mode == 3 && dlt[1][0] != 0) return "internal: mode 3 with the tens digit in the outer word";
   if (mode == 4 && dlt[1][0] == 0) return "internal: mode 4 without the tens digit in the outer word";
   FastArgs fa;
@@ -251,6 +264,8 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
     Ln.blocks = (uint32_t)((cnt + kBlock - 1) / kBlock);
     Ln.nonces = cnt * fa.kpow;
     Ln.btail = Y.nb;
+    Ln.Y = Y;
+    if (mode == 5) memcpy(Ln.tabw, tmpl + 16, sizeof Ln.tabw);
     Ln.fa.part_off = plan.total_blocks;
     plan.total_blocks += Ln.blocks;
     plan.total_nonces += Ln.nonces;
@@ -259,6 +274,30 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
     cur += cnt;
   }
   return std::string();
+}
+
+// MODE 5 table of a launch: 10^k rows of 64 words, row c for lo value c:
+// row[0] = W[0] (round 0's per-thread half already holds K[0]), row[t] =
+// K[t] + W[t] for t >= 1, W = tail block 1 with c's k digits in place.
+inline std::vector<uint32_t> build_kwtable(const Launch& L) {
+  const int k = L.Y.k;
+  const int qv = L.Y.q - 64;
+  const uint32_t rows = (uint32_t)pow10u(k);
+  std::vector<uint32_t> tab((size_t)rows * 64u);
+  for (uint32_t c = 0; c < rows; ++c) {
+    uint32_t w[64];
+    for (int i = 0; i < 16; ++i) w[i] = L.tabw[i];
+    uint32_t x = c;
+    for (int j = 0; j < k; ++j, x /= 10u) {
+      const int p = qv - j;  // byte of the 10^j digit
+      w[p >> 2] += (x % 10u) << (24 - 8 * (p & 3));
+    }
+    for (int t = 16; t < 64; ++t) w[t] = sched(w, t);
+    uint32_t* row = tab.data() + (size_t)c * 64u;
+    row[0] = w[0];
+    for (int t = 1; t < 64; ++t) row[t] = k256(t) + w[t];
+  }
+  return tab;
 }
 
 // Build the launch list for [lower, upper] (inclusive); lower <= upper.

@@ -56,6 +56,7 @@ struct FastArgs {
   uint32_t dt[2];     // tens carry:     (tens delta) - 10 * du
   uint32_t dhd[2];    // hundreds carry: (hundreds delta) - 10 * (tens delta)
   uint32_t part_off;  // first partial slot of this launch
+  uint64_t kwtab;     // MODE 5: 10^k rows of 64 words (row[0] = W[0], row[t] = K[t] + W[t])
 };
 
 // Arguments of the generic kernel (one nonce per thread, any layout).
@@ -347,10 +348,59 @@ P1_HD uint32_t uniform_word(const FastArgs& A, int i) {  // the tail word after 
 //   2  in words FV and FV+1, both updated per nonce (NV = 2)
 //   3  hundreds in FV, tens and units in FV+1: split, W[FV] work per 100 nonces
 //   4  hundreds and tens in FV, units in FV+1: split, W[FV] work per 10 nonces
-P1_HD constexpr int mode_nv(int mode) { return mode == 1 ? 1 : 2; }
+//   5  uniform block: PRE layout whose variable block (tail block 1) holds
+//      only the k lo digits and constants (tail bytes 64..q, k = q - 63 <= 4)
+P1_HD constexpr int mode_nv(int mode) { return mode == 2 || mode == 3 || mode == 4 ? 2 : 1; }
+
+// A word of a wave-uniform table row: a scalar load on the device (constant
+// address space: the table is read-only for the whole launch).
+P1_HD uint32_t ld_uniform(const uint32_t* p, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return ((const __attribute__((address_space(4))) uint32_t*)p)[i];
+#else
+  return p[i];
+#endif
+}
+
+// MODE 5.  Every word of the variable block is a lo digit or a launch
+// constant, so its whole message schedule depends on the lo value alone --
+// the same for every thread of the launch at a given loop step.  The host
+// tabulates it once per launch (FastArgs::kwtab: row c = lo value c), and the
+// per-nonce loop is the 64 rounds with K[t] + W[t] read from the row by
+// scalar loads into SGPRs: no schedule work at all.  Round 0's per-thread
+// half is hoisted (row[0] is W[0] alone).  The chaining value entering the
+// block is the thread's PRE block (hi digits), computed once per 10^k nonces.
+P1_HD Key fast_thread_uniform(const FastArgs& A, uint32_t tid) {
+  FastSetup S;
+  fast_setup(A, tid, S);
+  State s0, s1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s0.v[i] = S.cv[i];
+  round_half<0>(s0, s1);
+  const uint32_t* tab = (const uint32_t*)(uintptr_t)A.kwtab;
+  uint64_t best = ~0ull;
+  uint32_t bestc = 0;
+  for (uint32_t c = 0; c < A.kpow; ++c) {
+    const uint32_t* row = tab + (size_t)c * 64u;
+    State s = s1;
+    const uint32_t w0 = ld_uniform(row, 0);
+    s.v[0] = add2(s.v[0], w0);
+    s.v[4] = add2(s.v[4], w0);
+#pragma unroll
+    for (int t = 1; t < 64; ++t) sha_round(s, ld_uniform(row, (uint32_t)t));
+    const uint64_t h = ((uint64_t)(S.cv[0] + s.v[0]) << 32) | (uint64_t)(S.cv[1] + s.v[1]);
+    const bool lt = h < best;  // strict '<': first minimum wins (miner.go:59)
+    best = lt ? h : best;
+    bestc = lt ? c : bestc;
+  }
+  Key k;
+  k.h = S.valid ? best : ~0ull;
+  k.n = S.valid ? S.hi * (uint64_t)A.kpow + bestc : ~0ull;
+  return k;
+}
 
 template <int FV, int MODE, bool TRAIL>
-P1_HD Key fast_thread(const FastArgs& A, uint32_t tid) {
+P1_HD Key fast_thread_digits(const FastArgs& A, uint32_t tid) {
   constexpr int NV = mode_nv(MODE);
   FastSetup S;
   fast_setup(A, tid, S);
@@ -409,6 +459,16 @@ P1_HD Key fast_thread(const FastArgs& A, uint32_t tid) {
   k.h = S.valid ? best : ~0ull;
   k.n = S.valid ? S.hi * (uint64_t)A.kpow + bestc : ~0ull;
   return k;
+}
+
+template <int FV, int MODE, bool TRAIL>
+P1_HD Key fast_thread(const FastArgs& A, uint32_t tid) {
+  if constexpr (MODE == 5) {
+    static_assert(FV == 0 && !TRAIL, "MODE 5 is the whole tail block 1");
+    return fast_thread_uniform(A, tid);
+  } else {
+    return fast_thread_digits<FV, MODE, TRAIL>(A, tid);
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -91,14 +91,20 @@ def test_emu_every_layout_k3(oracle_mod, nosplit):
     seen = set()
     for L in range(0, 128):
         m = bytes(rnd.randrange(32, 127) for _ in range(L))
-        for d in (5, 9, 10, 11, 12, 20):
+        for d in (4, 5, 9, 10, 11, 12, 20):
             b = 10 ** (d - 1)
-            lo = b + rnd.randrange(0, 10**4) if d < 20 else b
-            hi = min(lo + 4999, U64_MAX)
+            # d = 4 with (L + 1) % 64 == 0 is the 1-block <0,1> layout
+            lo = b + rnd.randrange(0, 3000 if d == 4 else 10**4) if d < 20 else b
+            # a MODE 5 layout with 4 digits in tail block 1 loops over 10^4
+            # nonces per thread: give it two whole blocks
+            four = (L + 1) % 64 + d - 1 == 67
+            hi = min(lo + (24999 if four else 4999), U64_MAX)
             got, nf, _ = emu(m, lo, hi, minthreads=1, nosplit=nosplit, variants=seen)
             assert nf >= 1
             assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
-    want = {v for v in all_variants(True) if (v[1] == 2) == nosplit or v[1] == 1}
+    # mode 1 and MODE 5 (uniform tail block 1) run in both passes; modes 3/4
+    # only with split, mode 2 only with nosplit
+    want = {v for v in all_variants(True) if (v[1] == 2) == nosplit or v[1] in (1, 5)}
     assert seen == want, sorted(want ^ seen)
 
 

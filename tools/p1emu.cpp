@@ -36,7 +36,13 @@ static Key run_fast(const FastArgs& A, uint64_t threads) {
   return best;
 }
 
-static Key dispatch_fast(const Launch& L) {
+static Key dispatch_fast(const Launch& L0) {
+  Launch L = L0;
+  std::vector<uint32_t> tab;  // MODE 5: the K+W table, here in host memory
+  if (L.mode == 5) {
+    tab = build_kwtable(L);
+    L.fa.kwtab = (uint64_t)(uintptr_t)tab.data();
+  }
 #define P1_CASE(FV, MODE, TR) \
   if (L.fv == FV && L.mode == MODE && L.trail == TR) return run_fast<FV, MODE, TR>(L.fa, L.threads);
 #include "../p1_amd/csrc/fast_variants.inc"
