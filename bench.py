@@ -422,7 +422,9 @@ def main():
             if roofline["frac"] > 1.0:
                 roofline["executed"]["why_alg_frac_above_1"] = (
                     "the algorithmic count charges both tail blocks per nonce (SURVEY.md 8(d)); the kernel "
-                    "computes the hi-digit block once per 10^3 nonces (PRE) and executes ~1 block per nonce")
+                    "compresses the hi-digit block once per 10^k nonces (PRE) and, where the second block "
+                    "holds only lo digits (MODE 5), reads that block's whole message schedule from a "
+                    "per-launch table, so per nonce it executes the 64 rounds of one block and no schedule")
         mix = mix_roofline()
         if mix and k_ms > 0:
             mix["peak_GH_s"] = mix["peak_GH_s_per_block"] / cfg["b_tail"]
