@@ -343,9 +343,13 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
   t.k = L.Y.k;
   t.dptr = nullptr;
   HIPCHK(hipMalloc(&t.dptr, tab.size() * sizeof(uint32_t)));
+  hipError_t e = hipMemcpyAsync(t.dptr, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(d.stream);  // `tab` is freed on return
+  if (e != hipSuccess) {  // never cache a table that did not arrive whole
+    (void)hipFree(t.dptr);
+    return fail(P1HIP_ERR_HIP, std::string("K+W table upload: ") + hipGetErrorString(e));
+  }
   d.kwtabs.push_back(t);
-  HIPCHK(hipMemcpyAsync(t.dptr, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
-  HIPCHK(hipStreamSynchronize(d.stream));  // `tab` is freed on return
   *dptr = (uint64_t)(uintptr_t)t.dptr;
   return P1HIP_OK;
 }
