@@ -143,10 +143,14 @@ struct Runtime {
   //                           (exercises the multi-device error path)
   //   P1HIP_MAX_LAUNCH_BLOCKS workgroups per k_scan launch (read per scan,
   //                           launch_block_limit)
+  //   P1HIP_NO_TABLE          no MODE 5: layouts whose tail block 1 holds only
+  //                           lo digits run the digit-update variants (A/B,
+  //                           and a second kernel path to cross-check MODE 5)
   //   P1HIP_NO_SPLIT          straddling lo digits use mode 2 instead of the
   //                           split modes (A/B builds with -DP1_NV2_PLAIN)
   uint64_t min_fast_threads = kMinFastThreads;
   bool split = true;
+  bool tabulate = true;
   int fail_device = -1;
   p1hip_stats_t stats{};
 };
@@ -246,6 +250,8 @@ int init_devs(Runtime& R, const std::vector<int>& ords) {
   R.min_fast_threads = mft && *mft ? strtoull(mft, nullptr, 10) : kMinFastThreads;
   const char* nsp = getenv("P1HIP_NO_SPLIT");
   R.split = !(nsp && nsp[0] == '1');
+  const char* ntb = getenv("P1HIP_NO_TABLE");
+  R.tabulate = !(ntb && ntb[0] == '1');
   const char* fdev = getenv("P1HIP_TEST_FAIL_DEVICE");
   R.fail_device = fdev && *fdev ? atoi(fdev) : -1;
   if ((nd > 1 || R.rccl_one) && R.use_rccl) {
@@ -356,13 +362,13 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
 
 // Run one device's share [lo, hi] (lo <= hi) and leave its Key in d.d_res.
 int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, bool profiling,
-              uint64_t min_fast_threads, bool split) {
+              uint64_t min_fast_threads, bool split, bool tabulate) {
   HIPCHK(hipSetDevice(d.ordinal));
   d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
   d.scan_launches = d.scan_nonces = d.scan_ops = 0;
   d.fast_ms = d.scan_ms = 0.0;
   Plan plan;
-  std::string err = make_plan(msg, len, lo, hi, plan, true, min_fast_threads, split);
+  std::string err = make_plan(msg, len, lo, hi, plan, true, min_fast_threads, split, tabulate);
   if (!err.empty()) return fail(P1HIP_ERR_ARGS, "planner: " + err);
   // Longest-running workgroups first: fast pieces by lo-loop length (10^k),
   // then generic pieces, so short work fills the grid's drain.
@@ -575,7 +581,7 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
         d.small_used = true;
         r = run_small(d, msg, msg_len, slo[i], shi[i], !coll && nd == 1, R.profiling);
       } else if (active[i]) {
-        r = run_range(d, msg, msg_len, slo[i], shi[i], R.profiling, R.min_fast_threads, R.split);
+        r = run_range(d, msg, msg_len, slo[i], shi[i], R.profiling, R.min_fast_threads, R.split, R.tabulate);
       } else {
         // empty shard: contribute the identity key (all ones)
         if (hipSetDevice(d.ordinal) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipSetDevice");

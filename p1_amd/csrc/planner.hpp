@@ -83,17 +83,23 @@ struct Layout {
   int vb;     // fast path: tail block holding the lo digits
   int k;      // fast path: lo digits per thread loop
   bool trail; // fast path: a constant block follows block vb
+  bool tab;   // MODE 5 allowed (tabulated block-1 schedule)
 };
 
-inline Layout make_layout(uint32_t r, int d) {
+// `tabulate` = false keeps layouts whose block 1 holds only lo digits on
+// the digit-update variants (k = 3 or q - 63, MODE 1) instead of MODE 5:
+// the A/B and cross-check path of P1HIP_NO_TABLE.
+inline Layout make_layout(uint32_t r, int d, bool tabulate = true) {
   Layout Y;
   Y.d = d;
+  Y.tab = tabulate;
   Y.q = (int)r + d - 1;
   Y.nb = ((int)r + d + 9 <= 64) ? 1 : 2;
   if (Y.nb == 1) { Y.vb = 0; Y.k = 3; Y.trail = false; }
   else if (Y.q <= 63) { Y.vb = 0; Y.k = 3; Y.trail = true; }     // lo digits in block 0
-  else if (Y.q - 63 <= 4) { Y.vb = 1; Y.k = Y.q - 63; Y.trail = false; } // every block-1 digit lo: MODE 5
-  else { Y.vb = 1; Y.k = 3; Y.trail = false; }                          // lo digits in block 1
+  else if (tabulate && Y.q - 63 <= 4) { Y.vb = 1; Y.k = Y.q - 63; Y.trail = false; } // all block-1 digits lo: MODE 5
+  else if (Y.q - 64 >= 2) { Y.vb = 1; Y.k = 3; Y.trail = false; }                // lo digits in block 1
+  else { Y.vb = 1; Y.k = Y.q - 63; Y.trail = false; }                            // q in {64,65}: k = 1, 2
   return Y;
 }
 
@@ -179,7 +185,7 @@ struct Variant {
 inline Variant fast_variant(const Layout& Y, bool split = true) {
   const int qv = Y.q - 64 * Y.vb;
   Variant v;
-  if (Y.vb == 1 && Y.q - 63 == Y.k) {  // tail block 1 holds only lo digits (in W[0]) and constants
+  if (Y.tab && Y.vb == 1 && Y.q - 63 == Y.k) {  // tail block 1 holds only lo digits (in W[0]) and constants
     v.fv = 0;
     v.nv = 1;
     v.mode = 5;
@@ -306,7 +312,8 @@ inline std::vector<uint32_t> build_kwtable(const Launch& L) {
 // tests pass 1 so that k = 3 (and the NV = 2, PRE and TRAIL variants it
 // selects) is exercised on ranges the oracle finishes in seconds.
 inline std::string make_plan(const uint8_t* msg, size_t L, uint64_t lower, uint64_t upper, Plan& plan,
-                             bool fast_ok = true, uint64_t min_fast_threads = kMinFastThreads, bool split = true) {
+                             bool fast_ok = true, uint64_t min_fast_threads = kMinFastThreads, bool split = true,
+                             bool tabulate = true) {
   Prefix P;
   make_prefix(msg, L, P);
   plan = Plan();
@@ -316,7 +323,7 @@ inline std::string make_plan(const uint8_t* msg, size_t L, uint64_t lower, uint6
     const uint64_t s = lower > dlo ? lower : dlo;
     const uint64_t e = upper < dhi ? upper : dhi;
     if (s > e) continue;
-    Layout Y = make_layout(P.r, d);
+    Layout Y = make_layout(P.r, d, tabulate);
     // smaller k keeps the lo digits inside the same block (they are a suffix
     // of make_layout's k digits), so any k <= Y.k is a valid layout
     while (Y.k > 1 && (e - s) / pow10u(Y.k) + 1 < min_fast_threads) --Y.k;

@@ -38,7 +38,8 @@ def reinit(gpu, monkeypatch):
         return gpu
 
     yield go
-    for k in ("P1HIP_MIN_FAST_THREADS", "P1HIP_FORCE_RCCL", "P1HIP_TEST_FAIL_DEVICE", "P1HIP_NO_RCCL"):
+    for k in ("P1HIP_MIN_FAST_THREADS", "P1HIP_FORCE_RCCL", "P1HIP_TEST_FAIL_DEVICE", "P1HIP_NO_RCCL",
+              "P1HIP_NO_TABLE"):
         monkeypatch.delenv(k, raising=False)
     gpu.shutdown()
     gpu.init_devices([0])
@@ -73,6 +74,36 @@ def test_k3_straddles_and_edges(reinit, oracle_mod):
             assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (L, d)
     for m in (b"msg", b"y" * 61):
         assert g.scan(m, U64_MAX - 7000, U64_MAX) == oracle_mod.scan(m, U64_MAX - 7000, U64_MAX, threads=8)
+
+
+def test_mode5_cross_check_full_size(reinit, oracle_mod):
+    """MODE 5 (tail block 1 holds only lo digits; its schedule read from a
+    per-launch K+W table) against the digit-update variants the same layouts
+    run under P1HIP_NO_TABLE=1: two independent kernel paths must agree on
+    configs[2]'s whole [0, 2^34) and on 10^7-nonce ranges of every MODE 5
+    layout class (1..4 digits in block 1, k = 1..4), and the small ones also
+    against the oracle."""
+    rnd = random.Random(34)
+    cases = [(b"cmu440-p1-" * 12, 0, (1 << 34) - 1)]
+    for blk1 in (1, 2, 3, 4):               # digits in tail block 1 (q - 63)
+        for r in (45, 50, 57, 63):          # (L + 1) % 64
+            d = blk1 + 64 - r
+            if not 1 <= d <= 20:
+                continue
+            m = bytes(rnd.randrange(32, 127) for _ in range(r - 1 + 64 * rnd.randrange(0, 2)))
+            lo = 10 ** (d - 1) + rnd.randrange(0, min(10**6, (10**d - 10 ** (d - 1)) // 2))
+            cases.append((m, lo, min(lo + 10**7, 10**d - 1, U64_MAX)))
+    g = reinit(P1HIP_NO_TABLE=1)
+    want = [g.scan(m, lo, hi) for m, lo, hi in cases]
+    g = reinit()
+    g.reset_stats()
+    got = [g.scan(m, lo, hi) for m, lo, hi in cases]
+    assert got == want
+    assert oracle_mod.hash(cases[0][0], got[0][1]) == got[0][0]
+    for (m, lo, hi), key in zip(cases[1:], got[1:]):
+        assert oracle_mod.hash(m, key[1]) == key[0]
+        small_hi = lo + 20000
+        assert g.scan(m, lo, small_hi) == oracle_mod.scan(m, lo, small_hi, threads=8)
 
 
 def test_rccl_allgather_one_device(reinit, oracle_mod):

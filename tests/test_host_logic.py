@@ -15,12 +15,14 @@ U64_MAX = (1 << 64) - 1
 EMU = os.path.join(ROOT, "tools", "p1emu")
 
 
-def emu(msg, lo, hi, generic=False, minthreads=None, nosplit=False, variants=None):
+def emu(msg, lo, hi, generic=False, minthreads=None, nosplit=False, variants=None, notable=False):
     args = [EMU, msg.hex() if msg else "-", str(lo), str(hi)] + (["generic"] if generic else [])
     if minthreads is not None:
         args.append(f"minthreads={minthreads}")
     if nosplit:
         args.append("nosplit")
+    if notable:
+        args.append("notable")
     out = subprocess.run(args, capture_output=True, text=True, check=True).stdout.split()
     if variants is not None and out[4] != "-":
         variants.update(tuple(int(x) for x in v.split(":")) for v in out[4].split(","))
@@ -79,8 +81,9 @@ def test_emu_every_layout(oracle_mod):
             assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
 
 
-@pytest.mark.parametrize("nosplit", [False, True], ids=["split", "plain2"])
-def test_emu_every_layout_k3(oracle_mod, nosplit):
+@pytest.mark.parametrize("nosplit,notable", [(False, False), (True, False), (False, True)],
+                         ids=["split", "plain2", "notable"])
+def test_emu_every_layout_k3(oracle_mod, nosplit, notable):
     """Planner occupancy floor at 1 thread: k = 3 on small ranges, so every
     (FV, MODE, TRAIL) variant, PRE/TRAIL at k = 3 and the tens/hundreds carry
     deltas (dt/dhd) are replayed against the oracle.  The
@@ -99,12 +102,13 @@ def test_emu_every_layout_k3(oracle_mod, nosplit):
             # nonces per thread: give it two whole blocks
             four = (L + 1) % 64 + d - 1 == 67
             hi = min(lo + (24999 if four else 4999), U64_MAX)
-            got, nf, _ = emu(m, lo, hi, minthreads=1, nosplit=nosplit, variants=seen)
+            got, nf, _ = emu(m, lo, hi, minthreads=1, nosplit=nosplit, variants=seen, notable=notable)
             assert nf >= 1
             assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
-    # mode 1 and MODE 5 (uniform tail block 1) run in both passes; modes 3/4
-    # only with split, mode 2 only with nosplit
-    want = {v for v in all_variants(True) if (v[1] == 2) == nosplit or v[1] in (1, 5)}
+    # mode 1 runs in every pass, MODE 5 (tabulated tail block 1) unless
+    # notable; modes 3/4 only with split, mode 2 only with nosplit
+    want = {v for v in all_variants(True)
+            if (v[1] == 2) == nosplit and v[1] != 5 or v[1] == 1 or (v[1] == 5 and not notable)}
     assert seen == want, sorted(want ^ seen)
 
 

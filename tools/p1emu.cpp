@@ -7,10 +7,11 @@
 // CPU-only test suite.  It is never part of libp1hip.so and never used to
 // produce a product result.
 //
-// usage: p1emu <msg-hex> <lower> <upper> [generic | minthreads=N] [nosplit]
+// usage: p1emu <msg-hex> <lower> <upper> [generic | minthreads=N] [nosplit] [notable]
 //   minthreads=N sets the planner's occupancy floor (1 keeps k = 3 on small
 //   ranges, so every k = 3 variant is replayed); nosplit uses mode 2 for
-//   straddling lo digits (p1emu is built with -DP1_NV2_PLAIN)
+//   straddling lo digits (p1emu is built with -DP1_NV2_PLAIN); notable keeps
+//   layouts whose tail block 1 holds only lo digits off MODE 5
 //   prints "<hash> <nonce> <fast_launches> <generic_launches> <variants>"
 //   where <variants> lists the fast variants run as FV:MODE:TRAIL,... ("-"
 //   when none)
@@ -72,17 +73,18 @@ int main(int argc, char** argv) {
   const uint64_t upper = strtoull(argv[3], nullptr, 10);
   const bool generic_only = argc > 4 && strcmp(argv[4], "generic") == 0;
   uint64_t min_threads = kMinFastThreads;
-  bool split = true;
+  bool split = true, tabulate = true;
   for (int i = 4; i < argc; ++i) {
     if (strncmp(argv[i], "minthreads=", 11) == 0) min_threads = strtoull(argv[i] + 11, nullptr, 10);
     if (strcmp(argv[i], "nosplit") == 0) split = false;
+    if (strcmp(argv[i], "notable") == 0) tabulate = false;
   }
   Key best = {~0ull, ~0ull};
   int nf = 0, ng = 0;
   std::string vars;
   if (lower <= upper) {
     Plan plan;
-    std::string err = make_plan(msg.data(), msg.size(), lower, upper, plan, !generic_only, min_threads, split);
+    std::string err = make_plan(msg.data(), msg.size(), lower, upper, plan, !generic_only, min_threads, split, tabulate);
     if (!err.empty()) {
       fprintf(stderr, "plan error: %s\n", err.c_str());
       return 1;
