@@ -376,7 +376,7 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
   for (size_t i = 0; i < order.size(); ++i) order[i] = i;
   auto weight = [&](size_t i) -> uint64_t {
     const Launch& L = plan.launches[i];
-    return L.fast ? (uint64_t)L.fa.kpow * (uint64_t)L.btail : (uint64_t)L.btail - 1;
+    return L.fast ? (uint64_t)(L.fa.kpow / L.fa.nsub) * (uint64_t)L.btail : (uint64_t)L.btail - 1;
   };
   std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return weight(a) > weight(b); });
   // Pack into launches of <= kMaxSegs segments / kMaxLaunchBlocks workgroups.

@@ -218,8 +218,10 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
     const bool is_len = (!Y.trail && i == 15);
     if (!is_len && vw[i] != 0u) return "internal: unexpected non-zero tail word";
   }
+  // the digit-update modes handle k <= 3; only MODE 5 (tabulated) takes k = 4
+  if (k > 3 && var.mode != 5) return "internal: more than 3 lo digits outside MODE 5";
   uint32_t dlt[3][2] = {{0, 0}, {0, 0}, {0, 0}};  // per lo digit (units, tens, hundreds)
-  for (int t = 0; t < k; ++t) {
+  for (int t = 0; t < k && t < 3; ++t) {
     const int p = qv - t;
     const int slot = (p >> 2) - fv;
     dlt[t][slot] = 1u << (24 - 8 * (p & 3));
@@ -245,6 +247,7 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
   fa.p_last = (uint32_t)(Y.q - k);
   fa.pre = (uint32_t)Y.vb;
   fa.kpow = (uint32_t)pow10u(k);
+  fa.nsub = (mode == 5 && k > 3) ? (uint32_t)pow10u(k - 3) : 1u;
   fa.n1 = k >= 2 ? 10u : 1u;
   fa.n2 = k >= 3 ? 10u : 1u;
   for (int s = 0; s < 2; ++s) {
@@ -265,9 +268,10 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
     Ln.trail = Y.trail;
     Ln.fa = fa;
     Ln.fa.hi_first = cur;
-    Ln.fa.nthreads = (uint32_t)cnt;
-    Ln.threads = cnt;
-    Ln.blocks = (uint32_t)((cnt + kBlock - 1) / kBlock);
+    Ln.fa.nthreads = (uint32_t)cnt;  // hi values
+    // MODE 5 with nsub runs per hi: whole waves of 64 hi values per run
+    Ln.threads = fa.nsub > 1 ? (cnt + 63) / 64 * 64 * fa.nsub : cnt;
+    Ln.blocks = (uint32_t)((Ln.threads + kBlock - 1) / kBlock);
     Ln.nonces = cnt * fa.kpow;
     Ln.btail = Y.nb;
     Ln.Y = Y;
@@ -326,7 +330,8 @@ inline std::string make_plan(const uint8_t* msg, size_t L, uint64_t lower, uint6
     Layout Y = make_layout(P.r, d, tabulate);
     // smaller k keeps the lo digits inside the same block (they are a suffix
     // of make_layout's k digits), so any k <= Y.k is a valid layout
-    while (Y.k > 1 && (e - s) / pow10u(Y.k) + 1 < min_fast_threads) --Y.k;
+    // (a thread runs at most 10^3 nonces: MODE 5 splits k = 4 over 10 threads)
+    while (Y.k > 1 && (e - s) / pow10u(Y.k > 3 ? 3 : Y.k) + 1 < min_fast_threads) --Y.k;
     if (!fast_ok || d <= Y.k) {
       add_generic(P, Y, s, e, plan);
       continue;

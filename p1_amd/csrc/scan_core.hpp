@@ -57,6 +57,8 @@ struct FastArgs {
   uint32_t dhd[2];    // hundreds carry: (hundreds delta) - 10 * (tens delta)
   uint32_t part_off;  // first partial slot of this launch
   uint64_t kwtab;     // MODE 5: 10^k rows of 64 words (row[0] = W[0], row[t] = K[t] + W[t])
+  uint32_t nsub;      // MODE 5: threads per hi value (10^(k-3) for k > 3, else 1)
+  uint32_t pad_;
 };
 
 // Arguments of the generic kernel (one nonce per thread, any layout).
@@ -370,9 +372,30 @@ P1_HD uint32_t ld_uniform(const uint32_t* p, uint32_t i) {
 // scalar loads into SGPRs: no schedule work at all.  Round 0's per-thread
 // half is hoisted (row[0] is W[0] alone).  The chaining value entering the
 // block is the thread's PRE block (hi digits), computed once per 10^k nonces.
+// A value the caller knows to be the same in every lane of the wave, made
+// visibly uniform (an SGPR) for the compiler.
+P1_HD uint32_t wave_uniform(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+#else
+  return x;
+#endif
+}
+
+// With k = 4 the 10^4 lo values of a hi are split into nsub = 10 runs of
+// 1000 rows (the same thread length as k = 3, so a 2^32-nonce scan still has
+// thousands of workgroups).  The run index must be uniform per wave for the
+// row loads to stay scalar: wave w takes run w % nsub for 64 hi values
+// (planner: threads = ceil(his / 64) * 64 * nsub).  Each thread compresses
+// its hi's PRE block itself.
 P1_HD Key fast_thread_uniform(const FastArgs& A, uint32_t tid) {
+  const uint32_t wv = tid >> 6, lane = tid & 63u;
+  const uint32_t sub = wave_uniform(wv % A.nsub);
+  const uint32_t hid = (wv / A.nsub) * 64u + lane;
+  const uint32_t per = A.kpow / A.nsub;  // rows of this thread
+  const uint32_t c0 = sub * per;
   FastSetup S;
-  fast_setup(A, tid, S);
+  fast_setup(A, hid, S);
   State s0, s1;
 #pragma unroll
   for (int i = 0; i < 8; ++i) s0.v[i] = S.cv[i];
@@ -380,7 +403,7 @@ P1_HD Key fast_thread_uniform(const FastArgs& A, uint32_t tid) {
   const uint32_t* tab = (const uint32_t*)(uintptr_t)A.kwtab;
   uint64_t best = ~0ull;
   uint32_t bestc = 0;
-  for (uint32_t c = 0; c < A.kpow; ++c) {
+  for (uint32_t c = c0; c < c0 + per; ++c) {
     const uint32_t* row = tab + (size_t)c * 64u;
     State s = s1;
     const uint32_t w0 = ld_uniform(row, 0);
