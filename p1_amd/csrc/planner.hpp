@@ -15,7 +15,7 @@
 //      (one thread per nonce).
 //   3. the pieces become the segments of one multi-segment k_scan launch
 //      (p1hip.hip), longest-running workgroups first.
-// k is 3, except when the digits reach 1..4 bytes into the second tail block:
+// k is 3, except when the digits reach 1..5 bytes into the second tail block:
 // then k = that count, so that the block holds only lo digits (MODE 5, its
 // message schedule tabulated per lo value) and never a digit of block 0.
 #pragma once
@@ -36,6 +36,9 @@ constexpr uint64_t kAlgOpsPerCompression = 1384;
 // for that at k = 3 drop to k = 2 or 1 (shorter per-thread loops, more threads)
 // instead of running a few long waves on a mostly idle chip.
 constexpr uint64_t kMinFastThreads = 1ull << 18;
+// MODE 5 tabulates tail block 1's schedule for every lo value: at most 5
+// digits there (10^5 rows x 256 B = 25.6 MB per layout, cached per device).
+constexpr int kMaxTabDigits = 5;
 
 inline uint64_t pow10u(int e) {
   uint64_t v = 1;
@@ -97,7 +100,7 @@ inline Layout make_layout(uint32_t r, int d, bool tabulate = true) {
   Y.nb = ((int)r + d + 9 <= 64) ? 1 : 2;
   if (Y.nb == 1) { Y.vb = 0; Y.k = 3; Y.trail = false; }
   else if (Y.q <= 63) { Y.vb = 0; Y.k = 3; Y.trail = true; }     // lo digits in block 0
-  else if (tabulate && Y.q - 63 <= 4) { Y.vb = 1; Y.k = Y.q - 63; Y.trail = false; } // all block-1 digits lo: MODE 5
+  else if (tabulate && Y.q - 63 <= kMaxTabDigits) { Y.vb = 1; Y.k = Y.q - 63; Y.trail = false; }  // MODE 5
   else if (Y.q - 64 >= 2) { Y.vb = 1; Y.k = 3; Y.trail = false; }                // lo digits in block 1
   else { Y.vb = 1; Y.k = Y.q - 63; Y.trail = false; }                            // q in {64,65}: k = 1, 2
   return Y;
@@ -185,7 +188,7 @@ struct Variant {
 inline Variant fast_variant(const Layout& Y, bool split = true) {
   const int qv = Y.q - 64 * Y.vb;
   Variant v;
-  if (Y.tab && Y.vb == 1 && Y.q - 63 == Y.k) {  // tail block 1 holds only lo digits (in W[0]) and constants
+  if (Y.tab && Y.vb == 1 && Y.q - 63 == Y.k) {  // tail block 1 holds only lo digits (W[0], W[1]) and constants
     v.fv = 0;
     v.nv = 1;
     v.mode = 5;
@@ -218,7 +221,7 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
     const bool is_len = (!Y.trail && i == 15);
     if (!is_len && vw[i] != 0u) return "internal: unexpected non-zero tail word";
   }
-  // the digit-update modes handle k <= 3; only MODE 5 (tabulated) takes k = 4
+  // the digit-update modes handle k <= 3; only MODE 5 (tabulated) takes k = 4, 5
   if (k > 3 && var.mode != 5) return "internal: more than 3 lo digits outside MODE 5";
   uint32_t dlt[3][2] = {{0, 0}, {0, 0}, {0, 0}};  // per lo digit (units, tens, hundreds)
   for (int t = 0; t < k && t < 3; ++t) {
@@ -255,10 +258,13 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
     fa.dt[s] = dlt[1][s] - 10u * dlt[0][s];
     fa.dhd[s] = dlt[2][s] - 10u * dlt[1][s];
   }
+  // MODE 5 runs nsub threads per hi: cap the hi values so a piece stays
+  // within kMaxFastThreads threads (32-bit thread ids)
+  const uint64_t max_hi = kMaxFastThreads / fa.nsub;
   uint64_t cur = hs;
   for (;;) {
     const uint64_t left = he - cur;
-    const uint64_t cnt = left >= kMaxFastThreads ? kMaxFastThreads : left + 1;
+    const uint64_t cnt = left >= max_hi ? max_hi : left + 1;
     Launch Ln;
     memset(&Ln, 0, sizeof Ln);
     Ln.fast = true;

@@ -57,7 +57,7 @@ struct FastArgs {
   uint32_t dhd[2];    // hundreds carry: (hundreds delta) - 10 * (tens delta)
   uint32_t part_off;  // first partial slot of this launch
   uint64_t kwtab;     // MODE 5: 10^k rows of 64 words (row[0] = W[0], row[t] = K[t] + W[t])
-  uint32_t nsub;      // MODE 5: threads per hi value (10^(k-3) for k > 3, else 1)
+  uint32_t nsub;      // MODE 5: runs of 1000 rows per hi value (10^(k-3) for k > 3, else 1)
   uint32_t pad_;
 };
 
@@ -351,7 +351,7 @@ P1_HD uint32_t uniform_word(const FastArgs& A, int i) {  // the tail word after 
 //   3  hundreds in FV, tens and units in FV+1: split, W[FV] work per 100 nonces
 //   4  hundreds and tens in FV, units in FV+1: split, W[FV] work per 10 nonces
 //   5  uniform block: PRE layout whose variable block (tail block 1) holds
-//      only the k lo digits and constants (tail bytes 64..q, k = q - 63 <= 4)
+//      only the k lo digits and constants (tail bytes 64..q, k = q - 63 <= 5)
 P1_HD constexpr int mode_nv(int mode) { return mode == 2 || mode == 3 || mode == 4 ? 2 : 1; }
 
 // A word of a wave-uniform table row: a scalar load on the device (constant
@@ -382,10 +382,10 @@ P1_HD uint32_t wave_uniform(uint32_t x) {
 #endif
 }
 
-// With k = 4 the 10^4 lo values of a hi are split into nsub = 10 runs of
-// 1000 rows (the same thread length as k = 3, so a 2^32-nonce scan still has
-// thousands of workgroups).  The run index must be uniform per wave for the
-// row loads to stay scalar: wave w takes run w % nsub for 64 hi values
+// With k = 4 or 5 the 10^k lo values of a hi are split into nsub = 10^(k-3)
+// runs of 1000 rows (the same thread length as k = 3, so a 2^32-nonce scan
+// still has thousands of workgroups).  The run index must be uniform per wave
+// for the row loads to stay scalar: wave w takes run w % nsub for 64 hi values
 // (planner: threads = ceil(his / 64) * 64 * nsub).  Each thread compresses
 // its hi's PRE block itself.
 P1_HD Key fast_thread_uniform(const FastArgs& A, uint32_t tid) {

@@ -54,9 +54,10 @@ def test_k3_every_layout_vs_oracle(reinit, oracle_mod):
         for d in (4, 5, 9, 10, 11, 12, 20):
             b = 10 ** (d - 1)
             lo = b + rnd.randrange(0, 3000 if d == 4 else 10**4) if d < 20 else b
-            # MODE 5 with 4 digits in tail block 1 runs 10^4 nonces per thread
-            four = (L + 1) % 64 + d - 1 == 67
-            hi = min(lo + rnd.randrange(3000, 9000) + (20000 if four else 0), U64_MAX)
+            # MODE 5 with 4 / 5 digits in tail block 1 needs 10^4 / 10^5-aligned blocks
+            q = (L + 1) % 64 + d - 1
+            extra = {67: 20000, 68: 200000}.get(q, 0)
+            hi = min(lo + rnd.randrange(3000, 9000) + extra, U64_MAX)
             assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
     s = g.get_stats()
     # most nonces went through the fast (10^k loop) kernels, not the generic one
@@ -81,11 +82,11 @@ def test_mode5_cross_check_full_size(reinit, oracle_mod):
     per-launch K+W table) against the digit-update variants the same layouts
     run under P1HIP_NO_TABLE=1: two independent kernel paths must agree on
     configs[2]'s whole [0, 2^34) and on 10^7-nonce ranges of every MODE 5
-    layout class (1..4 digits in block 1, k = 1..4), and the small ones also
+    layout class (1..5 digits in block 1, k = 1..5), and the small ones also
     against the oracle."""
     rnd = random.Random(34)
     cases = [(b"cmu440-p1-" * 12, 0, (1 << 34) - 1)]
-    for blk1 in (1, 2, 3, 4):               # digits in tail block 1 (q - 63)
+    for blk1 in (1, 2, 3, 4, 5):            # digits in tail block 1 (q - 63)
         for r in (45, 50, 57, 63):          # (L + 1) % 64
             d = blk1 + 64 - r
             if not 1 <= d <= 20:

@@ -98,10 +98,10 @@ def test_emu_every_layout_k3(oracle_mod, nosplit, notable):
             b = 10 ** (d - 1)
             # d = 4 with (L + 1) % 64 == 0 is the 1-block <0,1> layout
             lo = b + rnd.randrange(0, 3000 if d == 4 else 10**4) if d < 20 else b
-            # a MODE 5 layout with 4 digits in tail block 1 loops over 10^4
-            # nonces per thread: give it two whole blocks
-            four = (L + 1) % 64 + d - 1 == 67
-            hi = min(lo + (24999 if four else 4999), U64_MAX)
+            # a MODE 5 layout with 4 / 5 digits in tail block 1 covers 10^4 /
+            # 10^5 nonces per hi: give it two whole blocks
+            q = (L + 1) % 64 + d - 1
+            hi = min(lo + {67: 24999, 68: 219999}.get(q, 4999), U64_MAX)
             got, nf, _ = emu(m, lo, hi, minthreads=1, nosplit=nosplit, variants=seen, notable=notable)
             assert nf >= 1
             assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
