@@ -403,7 +403,7 @@ inline double nonce_cycles(const Prefix& P, int d) {
   const Variant v = fast_variant(Y);
   double c = variant_cycles(v.fv, v.mode, Y.trail);
   if (c <= 0.0) c = 1384.0 * 3.6 * Y.nb;
-  return c + unhoisted / (double)pow10u(Y.k);
+  return c + unhoisted / (double)pow10u(Y.k > 3 ? 3 : Y.k);  // a thread runs <= 10^3 nonces
 }
 
 // Split [lower, upper] (inclusive, lower <= upper) into n >= 1 contiguous
