@@ -77,7 +77,9 @@ VALU_PEAK_PROFILE = "profiles/r01_valu_peak.jsonl"
 # profiles/r01v_valu_runs.jsonl: v_alignbit_b32 / v_add3_u32 streams 4.23,
 # full-rate VOP2 streams 2.13): a loop of A half-rate and B full-rate
 # instructions cannot issue in fewer than A x 4.23 + B x 2.13 SIMD cycles.
-VARIANT_PROFILE = "profiles/r02d_variant_report.jsonl"
+# per-variant loop mixes (tools/variant_report.py); later files add variants
+VARIANT_PROFILES = ["profiles/r02d_variant_report.jsonl", "profiles/r02k_variant_report_mode5.jsonl"]
+VARIANT_PROFILE = ", ".join(VARIANT_PROFILES)
 IDEAL_COST_A, IDEAL_COST_B = 4.23, 2.13
 
 
@@ -171,13 +173,15 @@ def fast_variant(msg_len, d, k=3):
 def workload_mix(msg_len, lo, hi):
     """Nonce-weighted loop mix (half-rate A, full-rate B VALU instructions per
     nonce) of the fast variants that scan [lo, hi]."""
-    path = os.path.join(ROOT, VARIANT_PROFILE)
-    if not os.path.exists(path):
-        return None
     table = {}
-    for line in open(path):
-        d = json.loads(line)
-        table[tuple(d["variant"])] = d["loop"]
+    for rel in VARIANT_PROFILES:
+        path = os.path.join(ROOT, rel)
+        if not os.path.exists(path):
+            return None
+        for line in open(path):
+            if line.startswith("{"):
+                d = json.loads(line)
+                table[tuple(d["variant"])] = d["loop"]
     a = b = w = 0.0
     for d in range(1, 21):
         dlo, dhi = (0 if d == 1 else 10 ** (d - 1)), 10 ** d - 1
