@@ -159,7 +159,7 @@ def fast_variant(msg_len, d, k=3):
         vb, trail = 0, False
     elif q <= 63:
         vb, trail = 0, True
-    elif q - 63 <= 5:
+    elif q - 63 <= 7:
         return 0, 5, False  # MODE 5: tail block 1 holds only the lo digits (k = q - 63)
     else:
         vb, trail = 1, False

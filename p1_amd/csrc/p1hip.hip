@@ -109,13 +109,13 @@ struct Dev {
   size_t seg_cap = 0;           // launch slots allocated
   ncclComm_t comm = nullptr;
   hipModule_t mod = nullptr;    // embedded code object, loaded on this device
-  hipFunction_t f_scan = nullptr, f_reduce = nullptr, f_pairs = nullptr, f_small = nullptr;
+  hipFunction_t f_scan = nullptr, f_reduce = nullptr, f_pairs = nullptr, f_small = nullptr, f_kwtable = nullptr;
   Key* d_small_part = nullptr;  // kSmallMaxBlocks partials of k_scan_small
   uint32_t* d_ticket = nullptr; // k_scan_small's last-workgroup counter (0 between scans)
   bool small_used = false;      // this scan ran k_scan_small (result already in h_res[0])
   std::vector<hipEvent_t> evs;  // profiling event pool (pairs)
-  // MODE 5 K+W tables on this device, most recent last (planner.hpp
-  // build_kwtable; keyed by the block-1 template and k)
+  // MODE 5 K+W tables on this device, least recently used first (built by
+  // k_kwtable; keyed by the block-1 template and k)
   struct KwTab {
     uint32_t w[16];
     int k;
@@ -229,6 +229,7 @@ int init_devs(Runtime& R, const std::vector<int>& ords) {
     HIPCHK(hipModuleGetFunction(&d.f_reduce, d.mod, "k_reduce"));
     HIPCHK(hipModuleGetFunction(&d.f_pairs, d.mod, "k_pairs"));
     HIPCHK(hipModuleGetFunction(&d.f_small, d.mod, "k_scan_small"));
+    HIPCHK(hipModuleGetFunction(&d.f_kwtable, d.mod, "k_kwtable"));
     HIPCHK(hipMalloc(&d.d_small_part, sizeof(Key) * kSmallMaxBlocks));
     HIPCHK(hipMalloc(&d.d_ticket, sizeof(uint32_t)));
     // on the library's own stream: a null-stream call would give every
@@ -330,30 +331,52 @@ int run_small(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
   return P1HIP_OK;
 }
 
-// Device copy of a MODE 5 launch's K+W table (cached: the same layout in
-// later scans reuses it; scans are synchronous, so an evicted table is idle).
+// Device copy of a MODE 5 launch's K+W table (cached, least recently used
+// evicted: the same layout in later scans reuses it; scans are synchronous,
+// so an evicted table is idle).
 constexpr size_t kMaxKwTabs = 8;
+// ... and at most this many bytes of them (a 7-digit table is 2.56 GB; one
+// scan needs at most one table per MODE 5 decade, < 2.9 GB in all)
+constexpr size_t kMaxKwTabBytes = (size_t)8 << 30;
 int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
-  for (Dev::KwTab& t : d.kwtabs)
+  for (size_t i = 0; i < d.kwtabs.size(); ++i) {
+    const Dev::KwTab t = d.kwtabs[i];
     if (t.k == L.Y.k && memcmp(t.w, L.tabw, sizeof t.w) == 0) {
+      // least recently used first: a scan touches at most 5 tables (one per
+      // MODE 5 decade), so it never evicts one it is about to launch with
+      d.kwtabs.erase(d.kwtabs.begin() + (long)i);
+      d.kwtabs.push_back(t);
       *dptr = (uint64_t)(uintptr_t)t.dptr;
       return P1HIP_OK;
     }
-  if (d.kwtabs.size() == kMaxKwTabs) {
+  }
+  const size_t need = (size_t)pow10u(L.Y.k) * 64u * sizeof(uint32_t);
+  for (;;) {
+    size_t held = 0;
+    for (const Dev::KwTab& t : d.kwtabs) held += (size_t)pow10u(t.k) * 64u * sizeof(uint32_t);
+    if (d.kwtabs.empty() || (d.kwtabs.size() < kMaxKwTabs && held + need <= kMaxKwTabBytes)) break;
     HIPCHK(hipFree(d.kwtabs.front().dptr));
     d.kwtabs.erase(d.kwtabs.begin());
   }
-  const std::vector<uint32_t> tab = build_kwtable(L);
+  // built on the device by k_kwtable, on the scan's stream (so the k_scan
+  // launch that reads it is ordered after it): no host work, no upload
   Dev::KwTab t;
   memcpy(t.w, L.tabw, sizeof t.w);
   t.k = L.Y.k;
   t.dptr = nullptr;
-  HIPCHK(hipMalloc(&t.dptr, tab.size() * sizeof(uint32_t)));
-  hipError_t e = hipMemcpyAsync(t.dptr, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(d.stream);  // `tab` is freed on return
-  if (e != hipSuccess) {  // never cache a table that did not arrive whole
+  const uint32_t rows = (uint32_t)pow10u(L.Y.k);
+  HIPCHK(hipMalloc(&t.dptr, (size_t)rows * 64u * sizeof(uint32_t)));
+  KwTableArgs a;
+  memset(&a, 0, sizeof a);
+  memcpy(a.tabw, L.tabw, sizeof a.tabw);
+  a.k = (uint32_t)L.Y.k;
+  a.qv = (uint32_t)(L.Y.q - 64);
+  a.rows = rows;
+  a.out = t.dptr;
+  const hipError_t e = launch(d.f_kwtable, (rows + kBlock - 1) / kBlock, kBlock, d.stream, a);
+  if (e != hipSuccess) {  // never cache a table that was not built
     (void)hipFree(t.dptr);
-    return fail(P1HIP_ERR_HIP, std::string("K+W table upload: ") + hipGetErrorString(e));
+    return fail(P1HIP_ERR_HIP, std::string("k_kwtable launch: ") + hipGetErrorString(e));
   }
   d.kwtabs.push_back(t);
   *dptr = (uint64_t)(uintptr_t)t.dptr;

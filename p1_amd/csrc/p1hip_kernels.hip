@@ -165,6 +165,17 @@ extern "C" __global__ __launch_bounds__(kBlock) void k_scan_small(SmallArgs a) {
   }
 }
 
+// MODE 5 table: row c = K + W of tail block 1 for lo value c
+extern "C" __global__ __launch_bounds__(kBlock) void k_kwtable(KwTableArgs a) {
+  const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+  if (c >= a.rows) return;
+  uint32_t row[64];
+  kwtable_row(a.tabw, (int)a.k, (int)a.qv, c, row);
+  uint4* out = (uint4*)(a.out + (size_t)c * 64u);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) out[i] = make_uint4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
+}
+
 // test hook: one crafted pair per thread -> per-workgroup partials
 extern "C" __global__ __launch_bounds__(kBlock) void k_pairs(const uint64_t* __restrict__ hs,
                                                              const uint64_t* __restrict__ ns, uint64_t n,

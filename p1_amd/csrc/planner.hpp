@@ -15,7 +15,7 @@
 //      (one thread per nonce).
 //   3. the pieces become the segments of one multi-segment k_scan launch
 //      (p1hip.hip), longest-running workgroups first.
-// k is 3, except when the digits reach 1..5 bytes into the second tail block:
+// k is 3, except when the digits reach 1..7 bytes into the second tail block:
 // then k = that count, so that the block holds only lo digits (MODE 5, its
 // message schedule tabulated per lo value) and never a digit of block 0.
 #pragma once
@@ -36,9 +36,14 @@ constexpr uint64_t kAlgOpsPerCompression = 1384;
 // for that at k = 3 drop to k = 2 or 1 (shorter per-thread loops, more threads)
 // instead of running a few long waves on a mostly idle chip.
 constexpr uint64_t kMinFastThreads = 1ull << 18;
-// MODE 5 tabulates tail block 1's schedule for every lo value: at most 5
-// digits there (10^5 rows x 256 B = 25.6 MB per layout, cached per device).
-constexpr int kMaxTabDigits = 5;
+// MODE 5 tabulates tail block 1's schedule for every lo value: at most 7
+// digits there (10^7 rows x 256 B = 2.56 GB per layout, built on the device
+// and cached there; measured 46.5 GH/s at 7 digits, 48.0 at 6, 48.9 at 5,
+// against 34 for the same layouts without a table).
+#ifndef P1_MAX_TAB_DIGITS
+#define P1_MAX_TAB_DIGITS 7  // A/B builds: make variant NAME=x HOSTEXTRA=-DP1_MAX_TAB_DIGITS=5
+#endif
+constexpr int kMaxTabDigits = P1_MAX_TAB_DIGITS;
 
 inline uint64_t pow10u(int e) {
   uint64_t v = 1;
@@ -221,7 +226,7 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
     const bool is_len = (!Y.trail && i == 15);
     if (!is_len && vw[i] != 0u) return "internal: unexpected non-zero tail word";
   }
-  // the digit-update modes handle k <= 3; only MODE 5 (tabulated) takes k = 4, 5
+  // the digit-update modes handle k <= 3; only MODE 5 (tabulated) takes k = 4..7
   if (k > 3 && var.mode != 5) return "internal: more than 3 lo digits outside MODE 5";
   uint32_t dlt[3][2] = {{0, 0}, {0, 0}, {0, 0}};  // per lo digit (units, tens, hundreds)
   for (int t = 0; t < k && t < 3; ++t) {
@@ -292,7 +297,8 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
   return std::string();
 }
 
-// MODE 5 table of a launch: 10^k rows of 64 words, row c for lo value c:
+// MODE 5 table of a launch on the host (tools/p1emu; the library builds it on
+// the device with k_kwtable): 10^k rows of 64 words, row c for lo value c:
 // row[0] = W[0] (round 0's per-thread half already holds K[0]), row[t] =
 // K[t] + W[t] for t >= 1, W = tail block 1 with c's k digits in place.
 inline std::vector<uint32_t> build_kwtable(const Launch& L) {
@@ -300,20 +306,36 @@ inline std::vector<uint32_t> build_kwtable(const Launch& L) {
   const int qv = L.Y.q - 64;
   const uint32_t rows = (uint32_t)pow10u(k);
   std::vector<uint32_t> tab((size_t)rows * 64u);
-  for (uint32_t c = 0; c < rows; ++c) {
-    uint32_t w[64];
-    for (int i = 0; i < 16; ++i) w[i] = L.tabw[i];
-    uint32_t x = c;
-    for (int j = 0; j < k; ++j, x /= 10u) {
-      const int p = qv - j;  // byte of the 10^j digit
-      w[p >> 2] += (x % 10u) << (24 - 8 * (p & 3));
-    }
-    for (int t = 16; t < 64; ++t) w[t] = sched(w, t);
-    uint32_t* row = tab.data() + (size_t)c * 64u;
-    row[0] = w[0];
-    for (int t = 1; t < 64; ++t) row[t] = k256(t) + w[t];
-  }
+  for (uint32_t c = 0; c < rows; ++c) kwtable_row(L.tabw, k, qv, c, tab.data() + (size_t)c * 64u);
   return tab;
+}
+
+// [s, e] inside one decade at layout Y: whole 10^k blocks as fast pieces,
+// the ragged edges generic -- except for MODE 5 at k > 3, whose edges (up to
+// 10^k - 1 nonces each) are planned again at the k = 3 digit layout, so only
+// < 10^3 nonces per edge end up one per thread.
+inline std::string add_pieces(const Prefix& P, const Layout& Y, uint64_t s, uint64_t e, Plan& plan, bool split) {
+  auto edge = [&](uint64_t a, uint64_t b) -> std::string {
+    if (Y.k <= 3) {
+      add_generic(P, Y, a, b, plan);
+      return std::string();
+    }
+    return add_pieces(P, make_layout(P.r, Y.d, false), a, b, plan, split);
+  };
+  const uint64_t B = pow10u(Y.k);
+  const uint64_t hs = s / B + (s % B != 0 ? 1u : 0u);
+  bool have = true;
+  uint64_t he = 0;
+  if (e % B == B - 1) he = e / B;
+  else if (e / B == 0) have = false;
+  else he = e / B - 1;
+  if (have && hs > he) have = false;
+  if (!have) return edge(s, e);
+  std::string err;
+  if (hs * B > s && !(err = edge(s, hs * B - 1)).empty()) return err;
+  if (!(err = add_fast(P, Y, hs, he, plan, split)).empty()) return err;
+  if (e % B != B - 1) return edge((he + 1) * B, e);
+  return std::string();
 }
 
 // Build the launch list for [lower, upper] (inclusive); lower <= upper.
@@ -335,29 +357,18 @@ inline std::string make_plan(const uint8_t* msg, size_t L, uint64_t lower, uint6
     if (s > e) continue;
     Layout Y = make_layout(P.r, d, tabulate);
     // smaller k keeps the lo digits inside the same block (they are a suffix
-    // of make_layout's k digits), so any k <= Y.k is a valid layout
-    // (a thread runs at most 10^3 nonces: MODE 5 splits k = 4 over 10 threads)
-    while (Y.k > 1 && (e - s) / pow10u(Y.k > 3 ? 3 : Y.k) + 1 < min_fast_threads) --Y.k;
+    // of make_layout's k digits), so any k <= Y.k is a valid layout; a thread
+    // runs at most 10^3 nonces (MODE 5 splits k > 3 into runs of 1000), so a
+    // MODE 5 layout that is too small goes straight to the k = 3 digit layout
+    if (Y.k > 3 && (e - s) / 1000u + 1 < min_fast_threads) Y = make_layout(P.r, d, false);
+    if (Y.k <= 3)
+      while (Y.k > 1 && (e - s) / pow10u(Y.k) + 1 < min_fast_threads) --Y.k;
     if (!fast_ok || d <= Y.k) {
       add_generic(P, Y, s, e, plan);
       continue;
     }
-    const uint64_t B = pow10u(Y.k);
-    const uint64_t hs = s / B + (s % B != 0 ? 1u : 0u);
-    bool have = true;
-    uint64_t he = 0;
-    if (e % B == B - 1) he = e / B;
-    else if (e / B == 0) have = false;
-    else he = e / B - 1;
-    if (have && hs > he) have = false;
-    if (!have) {
-      add_generic(P, Y, s, e, plan);
-      continue;
-    }
-    if (hs * B > s) add_generic(P, Y, s, hs * B - 1, plan);
-    std::string err = add_fast(P, Y, hs, he, plan, split);
+    std::string err = add_pieces(P, Y, s, e, plan, split);
     if (!err.empty()) return err;
-    if (e % B != B - 1) add_generic(P, Y, (he + 1) * B, e, plan);
   }
   return std::string();
 }

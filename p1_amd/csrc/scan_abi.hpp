@@ -26,6 +26,15 @@ struct Segment {
 
 constexpr int kReduceThreads = 1024;  // k_reduce: one workgroup
 
+// k_kwtable: builds a MODE 5 table on the device, one row per thread
+// (scan_core.hpp kwtable_row).
+struct KwTableArgs {
+  uint32_t tabw[16];  // tail block 1, '0' at the lo digit bytes
+  uint32_t k, qv, rows;
+  uint32_t pad_;
+  uint32_t* out;      // rows x 64 words
+};
+
 // Small scans (configs[0]-sized requests, single nonces of p1hip_hash): one
 // launch of k_scan_small with the whole plan in its kernel arguments (no
 // table copy), generic pieces only, and the grid's last workgroup folding the
@@ -51,4 +60,5 @@ struct SmallArgs {
 //   k_reduce(const Key* part, uint32_t n, Key* out)                  grid: 1 x kReduceThreads
 //   k_pairs(const uint64_t* hs, const uint64_t* ns, uint64_t n, Key* part)  grid: ceil(n/kBlock) x kBlock
 //   k_scan_small(SmallArgs a)                                        grid: a.nblocks x kBlock
+//   k_kwtable(KwTableArgs a)                                         grid: ceil(a.rows/kBlock) x kBlock
 }  // namespace p1

@@ -351,8 +351,35 @@ P1_HD uint32_t uniform_word(const FastArgs& A, int i) {  // the tail word after 
 //   3  hundreds in FV, tens and units in FV+1: split, W[FV] work per 100 nonces
 //   4  hundreds and tens in FV, units in FV+1: split, W[FV] work per 10 nonces
 //   5  uniform block: PRE layout whose variable block (tail block 1) holds
-//      only the k lo digits and constants (tail bytes 64..q, k = q - 63 <= 5)
+//      only the k lo digits and constants (tail bytes 64..q, k = q - 63 <= 7)
 P1_HD constexpr int mode_nv(int mode) { return mode == 2 || mode == 3 || mode == 4 ? 2 : 1; }
+
+// Row c of a MODE 5 table: tail block 1 (`tabw`, '0' at the lo digit bytes)
+// with c's k digits in place -- the 10^j digit at byte qv - j, always in
+// words 0..3 for the k <= 7 digits a table covers -- then row[0] = W[0] and
+// row[t] = K[t] + W[t].  The device builds tables with it (k_kwtable), the
+// host replay (tools/p1emu, planner.hpp build_kwtable) too.
+P1_HD void kwtable_row(const uint32_t tabw[16], int k, int qv, uint32_t c, uint32_t* row) {
+  uint32_t w[64];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w[i] = tabw[i];
+  uint32_t x = c;
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    if (j < k) {
+      const int p = qv - j;
+      const uint32_t v = (x % 10u) << (24 - 8 * (p & 3));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] += ((p >> 2) == i) ? v : 0u;  // no runtime-indexed array
+      x /= 10u;
+    }
+  }
+#pragma unroll
+  for (int t = 16; t < 64; ++t) w[t] = sched(w, t);
+  row[0] = w[0];
+#pragma unroll
+  for (int t = 1; t < 64; ++t) row[t] = k256(t) + w[t];
+}
 
 // A word of a wave-uniform table row: a scalar load on the device (constant
 // address space: the table is read-only for the whole launch).
@@ -382,7 +409,7 @@ P1_HD uint32_t wave_uniform(uint32_t x) {
 #endif
 }
 
-// With k = 4 or 5 the 10^k lo values of a hi are split into nsub = 10^(k-3)
+// With k = 4..7 the 10^k lo values of a hi are split into nsub = 10^(k-3)
 // runs of 1000 rows (the same thread length as k = 3, so a 2^32-nonce scan
 // still has thousands of workgroups).  The run index must be uniform per wave
 // for the row loads to stay scalar: wave w takes run w % nsub for 64 hi values

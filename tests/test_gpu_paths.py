@@ -56,7 +56,7 @@ def test_k3_every_layout_vs_oracle(reinit, oracle_mod):
             lo = b + rnd.randrange(0, 3000 if d == 4 else 10**4) if d < 20 else b
             # MODE 5 with 4 / 5 digits in tail block 1 needs 10^4 / 10^5-aligned blocks
             q = (L + 1) % 64 + d - 1
-            extra = {67: 20000, 68: 200000}.get(q, 0)
+            extra = {67: 20000, 68: 200000, 69: 2 * 10**6, 70: 2 * 10**7}.get(q, 0)
             hi = min(lo + rnd.randrange(3000, 9000) + extra, U64_MAX)
             assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
     s = g.get_stats()
@@ -77,26 +77,29 @@ def test_k3_straddles_and_edges(reinit, oracle_mod):
         assert g.scan(m, U64_MAX - 7000, U64_MAX) == oracle_mod.scan(m, U64_MAX - 7000, U64_MAX, threads=8)
 
 
-def test_mode5_cross_check_full_size(reinit, oracle_mod):
+def test_mode5_cross_check_full_size(reinit, oracle_mod, monkeypatch):
     """MODE 5 (tail block 1 holds only lo digits; its schedule read from a
     per-launch K+W table) against the digit-update variants the same layouts
     run under P1HIP_NO_TABLE=1: two independent kernel paths must agree on
     configs[2]'s whole [0, 2^34) and on 10^7-nonce ranges of every MODE 5
-    layout class (1..5 digits in block 1, k = 1..5), and the small ones also
+    layout class (1..7 digits in block 1, k = 1..7), and the small ones also
     against the oracle."""
     rnd = random.Random(34)
     cases = [(b"cmu440-p1-" * 12, 0, (1 << 34) - 1)]
-    for blk1 in (1, 2, 3, 4, 5):            # digits in tail block 1 (q - 63)
+    for blk1 in (1, 2, 3, 4, 5, 6, 7):      # digits in tail block 1 (q - 63)
         for r in (45, 50, 57, 63):          # (L + 1) % 64
             d = blk1 + 64 - r
             if not 1 <= d <= 20:
                 continue
             m = bytes(rnd.randrange(32, 127) for _ in range(r - 1 + 64 * rnd.randrange(0, 2)))
             lo = 10 ** (d - 1) + rnd.randrange(0, min(10**6, (10**d - 10 ** (d - 1)) // 2))
-            cases.append((m, lo, min(lo + 10**7, 10**d - 1, U64_MAX)))
-    g = reinit(P1HIP_NO_TABLE=1)
+            span = 3 * 10**7 if blk1 >= 6 else 10**7  # whole 10^k blocks inside
+            cases.append((m, lo, min(lo + span, 10**d - 1, U64_MAX)))
+    # occupancy floor 1: k is never lowered, so these ranges really run MODE 5
+    g = reinit(P1HIP_NO_TABLE=1, P1HIP_MIN_FAST_THREADS=1)
     want = [g.scan(m, lo, hi) for m, lo, hi in cases]
-    g = reinit()
+    monkeypatch.delenv("P1HIP_NO_TABLE")
+    g = reinit(P1HIP_MIN_FAST_THREADS=1)
     g.reset_stats()
     got = [g.scan(m, lo, hi) for m, lo, hi in cases]
     assert got == want
