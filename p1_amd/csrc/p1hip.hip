@@ -143,6 +143,8 @@ struct Runtime {
   //                           (exercises the multi-device error path)
   //   P1HIP_MAX_LAUNCH_BLOCKS workgroups per k_scan launch (read per scan,
   //                           launch_block_limit)
+  //   P1HIP_KWTAB_MAX_BYTES   MODE 5 table cap (read per scan; a larger table
+  //                           re-plans the share without MODE 5)
   //   P1HIP_NO_TABLE          no MODE 5: layouts whose tail block 1 holds only
   //                           lo digits run the digit-update variants (A/B,
   //                           and a second kernel path to cross-check MODE 5)
@@ -338,11 +340,15 @@ constexpr size_t kMaxKwTabs = 8;
 // ... and at most this many bytes of them (a 7-digit table is 2.56 GB; one
 // scan needs at most one table per MODE 5 decade, < 2.9 GB in all)
 constexpr size_t kMaxKwTabBytes = (size_t)8 << 30;
+// kNoTable: the table cannot be had (larger than the cap, or the device is
+// out of memory); the caller re-plans the share without MODE 5.
+constexpr int kNoTable = 1;
+
 int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
   for (size_t i = 0; i < d.kwtabs.size(); ++i) {
     const Dev::KwTab t = d.kwtabs[i];
     if (t.k == L.Y.k && memcmp(t.w, L.tabw, sizeof t.w) == 0) {
-      // least recently used first: a scan touches at most 5 tables (one per
+      // least recently used first: a scan touches at most 7 tables (one per
       // MODE 5 decade), so it never evicts one it is about to launch with
       d.kwtabs.erase(d.kwtabs.begin() + (long)i);
       d.kwtabs.push_back(t);
@@ -351,10 +357,14 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
     }
   }
   const size_t need = (size_t)pow10u(L.Y.k) * 64u * sizeof(uint32_t);
+  // P1HIP_KWTAB_MAX_BYTES (tests only): a lower cap, to exercise the re-plan
+  const char* capv = getenv("P1HIP_KWTAB_MAX_BYTES");
+  const size_t cap = capv && *capv ? (size_t)strtoull(capv, nullptr, 10) : kMaxKwTabBytes;
+  if (need > cap) return kNoTable;
   for (;;) {
     size_t held = 0;
     for (const Dev::KwTab& t : d.kwtabs) held += (size_t)pow10u(t.k) * 64u * sizeof(uint32_t);
-    if (d.kwtabs.empty() || (d.kwtabs.size() < kMaxKwTabs && held + need <= kMaxKwTabBytes)) break;
+    if (d.kwtabs.empty() || (d.kwtabs.size() < kMaxKwTabs && held + need <= cap)) break;
     HIPCHK(hipFree(d.kwtabs.front().dptr));
     d.kwtabs.erase(d.kwtabs.begin());
   }
@@ -365,7 +375,12 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
   t.k = L.Y.k;
   t.dptr = nullptr;
   const uint32_t rows = (uint32_t)pow10u(L.Y.k);
-  HIPCHK(hipMalloc(&t.dptr, (size_t)rows * 64u * sizeof(uint32_t)));
+  const hipError_t me = hipMalloc(&t.dptr, (size_t)rows * 64u * sizeof(uint32_t));
+  if (me == hipErrorOutOfMemory) {
+    (void)hipGetLastError();  // not sticky: clear it and scan without the table
+    return kNoTable;
+  }
+  HIPCHK(me);
   KwTableArgs a;
   memset(&a, 0, sizeof a);
   memcpy(a.tabw, L.tabw, sizeof a.tabw);
@@ -463,6 +478,8 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
         S.fa = L.fa;
         if (L.mode == 5) {
           const int rt = kwtable_for(d, L, &S.fa.kwtab);
+          if (rt == kNoTable)  // nothing launched yet: plan the share again without MODE 5
+            return run_range(d, msg, len, lo, hi, profiling, min_fast_threads, split, false);
           if (rt != P1HIP_OK) return rt;
         }
         d.fast_launches++;

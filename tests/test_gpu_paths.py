@@ -110,6 +110,21 @@ def test_mode5_cross_check_full_size(reinit, oracle_mod, monkeypatch):
         assert g.scan(m, lo, small_hi) == oracle_mod.scan(m, lo, small_hi, threads=8)
 
 
+def test_mode5_table_unavailable_replans(gpu, oracle_mod, monkeypatch):
+    """A MODE 5 table that cannot be had (here: larger than a test cap, in
+    production: device out of memory) makes the share re-plan without
+    MODE 5 instead of failing; the answer is unchanged."""
+    m = b"cmu440-p1-" * 12
+    cases = [(m, 10**10, 10**10 + 3 * 10**8), (m, 10**9 + 12345, 10**9 + 4 * 10**8)]
+    want = [gpu.scan(mm, lo, hi) for mm, lo, hi in cases]
+    monkeypatch.setenv("P1HIP_KWTAB_MAX_BYTES", "1000")
+    got = [gpu.scan(mm, lo, hi) for mm, lo, hi in cases]
+    monkeypatch.delenv("P1HIP_KWTAB_MAX_BYTES")
+    assert got == want
+    for (mm, lo, hi), (h, n) in zip(cases, got):
+        assert lo <= n <= hi and oracle_mod.hash(mm, n) == h
+
+
 def test_rccl_allgather_one_device(reinit, oracle_mod):
     g = reinit(P1HIP_FORCE_RCCL=1)
     for m, lo, hi in [(b"bradfitz", 0, 9999), (b"msg", 0, 2), (b"msg", 7, 3), (b"x" * 70, 10**9 - 3000, 10**9 + 3000)]:
