@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <exception>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -143,6 +144,7 @@ struct Runtime {
   //                           (exercises the multi-device error path)
   //   P1HIP_MAX_LAUNCH_BLOCKS workgroups per k_scan launch (read per scan,
   //                           launch_block_limit)
+  //   P1HIP_MAX_SCAN_SPAN     nonces per piece of a device's share (run_share)
   //   P1HIP_KWTAB_MAX_BYTES   MODE 5 table cap (read per scan; a larger table
   //                           re-plans the share without MODE 5)
   //   P1HIP_NO_TABLE          no MODE 5: layouts whose tail block 1 holds only
@@ -527,6 +529,42 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
   return P1HIP_OK;
 }
 
+// A device's share, in pieces of at most kMaxScanSpan nonces: the plan of a
+// share is O(its size / 2^26 hi values), so a share as large as the whole
+// u64 range (which the Go loop never finishes either) would need ~10^8
+// pieces.  Each piece is a full run_range; the keys are combined on the host
+// and the result written back to d.d_res.  Shares up to 2^40 nonces (about
+// 30 s of one GPU) are a single piece, with no extra copy.
+constexpr uint64_t kMaxScanSpan = 1ull << 40;
+int run_share(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, const Runtime& R) {
+  // P1HIP_MAX_SCAN_SPAN (tests only, read per scan): smaller pieces
+  const char* sv = getenv("P1HIP_MAX_SCAN_SPAN");
+  const uint64_t span = sv && *sv && strtoull(sv, nullptr, 10) > 0 ? strtoull(sv, nullptr, 10) : kMaxScanSpan;
+  if (hi - lo < span)
+    return run_range(d, msg, len, lo, hi, R.profiling, R.min_fast_threads, R.split, R.tabulate);
+  Key best = {~0ull, ~0ull};
+  uint64_t fl = 0, fn = 0, fo = 0, gl = 0, gn = 0, sl = 0, sn = 0, so = 0;
+  double fms = 0.0, sms = 0.0;
+  for (uint64_t a = lo;;) {
+    const uint64_t b = hi - a < span ? hi : a + (span - 1);
+    int r = run_range(d, msg, len, a, b, R.profiling, R.min_fast_threads, R.split, R.tabulate);
+    if (r != P1HIP_OK) return r;
+    Key k;
+    HIPCHK(hipMemcpyAsync(&k, d.d_res, sizeof(Key), hipMemcpyDeviceToHost, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    if (key_lt(k, best)) best = k;
+    fl += d.fast_launches; fn += d.fast_nonces; fo += d.fast_ops; gl += d.gen_launches; gn += d.gen_nonces;
+    sl += d.scan_launches; sn += d.scan_nonces; so += d.scan_ops; fms += d.fast_ms; sms += d.scan_ms;
+    if (b == hi) break;
+    a = b + 1;
+  }
+  d.fast_launches = fl; d.fast_nonces = fn; d.fast_ops = fo; d.gen_launches = gl; d.gen_nonces = gn;
+  d.scan_launches = sl; d.scan_nonces = sn; d.scan_ops = so; d.fast_ms = fms; d.scan_ms = sms;
+  HIPCHK(hipMemcpyAsync(d.d_res, &best, sizeof(Key), hipMemcpyHostToDevice, d.stream));
+  HIPCHK(hipStreamSynchronize(d.stream));  // `best` lives on this stack frame
+  return P1HIP_OK;
+}
+
 Key finish_key(Key k) {
   if (k.h == ~0ull) k.n = 0;  // identity (MaxUint64, 0) of miner.go:56
   return k;
@@ -621,7 +659,11 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
         d.small_used = true;
         r = run_small(d, msg, msg_len, slo[i], shi[i], !coll && nd == 1, R.profiling);
       } else if (active[i]) {
-        r = run_range(d, msg, msg_len, slo[i], shi[i], R.profiling, R.min_fast_threads, R.split, R.tabulate);
+        try {
+          r = run_share(d, msg, msg_len, slo[i], shi[i], R);
+        } catch (const std::exception& ex) {  // host allocation: never let it cross the C ABI
+          r = fail(P1HIP_ERR_HIP, std::string("host: ") + ex.what());
+        }
       } else {
         // empty shard: contribute the identity key (all ones)
         if (hipSetDevice(d.ordinal) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipSetDevice");

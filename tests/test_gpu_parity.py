@@ -207,3 +207,20 @@ def test_config4_range_on_one_gpu_multi_batch(gpu, oracle_mod, monkeypatch):
     a = gpu.scan("bradfitz", 0, (1 << 37) - 1)
     b = gpu.scan("bradfitz", 1 << 37, hi)
     assert min(a, b) == (h, n)
+
+
+def test_share_in_pieces(gpu, oracle_mod, monkeypatch):
+    """A device's share is scanned in pieces of at most 2^40 nonces (the plan
+    of one piece stays small however large the request); forced here to
+    pieces of 10^6 + 7 nonces, the answer and the nonce count are those of
+    the one-piece scan."""
+    cases = [("bradfitz", 10**9 - 3 * 10**6, 10**9 + 5 * 10**6), (b"cmu440-p1-" * 12, 10**10, 10**10 + 9 * 10**6)]
+    want = [gpu.scan(m, lo, hi) for m, lo, hi in cases]
+    monkeypatch.setenv("P1HIP_MAX_SCAN_SPAN", str(10**6 + 7))
+    for (m, lo, hi), w in zip(cases, want):
+        gpu.reset_stats()
+        assert gpu.scan(m, lo, hi) == w
+        assert gpu.get_stats()["scan_nonces"] == hi - lo + 1
+    monkeypatch.delenv("P1HIP_MAX_SCAN_SPAN")
+    for (m, lo, hi), (h, n) in zip(cases, want):
+        assert oracle_mod.hash(m, n) == h
