@@ -150,9 +150,15 @@ def test_multi_device_path_on_one_gpu(gpu, oracle_mod, monkeypatch):
                           (b"msg", 0, 1), (b"msg", 5, 5), (b"msg", 9, 3)]:
             assert gpu.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (m, lo, hi)
         assert gpu.scan("bradfitz", 0, (1 << 32) - 1) == (5256245051, 1626825724)
+        # MODE 5 on every "device" (each builds and caches its own K+W table),
+        # shards cut by p1hip_plan_shards
+        c3 = (b"cmu440-p1-" * 12, 10**10 - 2 * 10**9, 10**10 + 4 * 10**9)
+        got3 = gpu.scan(*c3)
     finally:
         monkeypatch.delenv("P1HIP_NO_RCCL")
         gpu.init_devices([0])
+    assert got3 == gpu.scan(*c3)
+    assert oracle_mod.hash(c3[0], got3[1]) == got3[0]
 
 
 def test_long_messages_and_limits(gpu, oracle_mod):
