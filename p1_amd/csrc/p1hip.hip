@@ -121,8 +121,10 @@ struct Dev {
     uint32_t w[16];
     int k;
     uint32_t* dptr;
+    uint64_t used_in;  // run_range call that last used it (never evicted during it)
   };
   std::vector<KwTab> kwtabs;
+  uint64_t range_id = 0;        // run_range calls on this device
   // per-scan accounting filled by run_range
   uint64_t fast_launches = 0, fast_nonces = 0, fast_ops = 0, gen_launches = 0, gen_nonces = 0;
   double fast_ms = 0.0;
@@ -348,8 +350,9 @@ constexpr int kNoTable = 1;
 
 int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
   for (size_t i = 0; i < d.kwtabs.size(); ++i) {
-    const Dev::KwTab t = d.kwtabs[i];
+    Dev::KwTab t = d.kwtabs[i];
     if (t.k == L.Y.k && memcmp(t.w, L.tabw, sizeof t.w) == 0) {
+      t.used_in = d.range_id;
       // least recently used first: a scan touches at most 7 tables (one per
       // MODE 5 decade), so it never evicts one it is about to launch with
       d.kwtabs.erase(d.kwtabs.begin() + (long)i);
@@ -367,8 +370,12 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
     size_t held = 0;
     for (const Dev::KwTab& t : d.kwtabs) held += (size_t)pow10u(t.k) * 64u * sizeof(uint32_t);
     if (d.kwtabs.empty() || (d.kwtabs.size() < kMaxKwTabs && held + need <= cap)) break;
-    HIPCHK(hipFree(d.kwtabs.front().dptr));
-    d.kwtabs.erase(d.kwtabs.begin());
+    // evict the least recently used table this share has not referenced yet
+    size_t v = 0;
+    while (v < d.kwtabs.size() && d.kwtabs[v].used_in == d.range_id) ++v;
+    if (v == d.kwtabs.size()) return kNoTable;  // everything held is in use by this share
+    HIPCHK(hipFree(d.kwtabs[v].dptr));
+    d.kwtabs.erase(d.kwtabs.begin() + (long)v);
   }
   // built on the device by k_kwtable, on the scan's stream (so the k_scan
   // launch that reads it is ordered after it): no host work, no upload
@@ -376,6 +383,7 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
   memcpy(t.w, L.tabw, sizeof t.w);
   t.k = L.Y.k;
   t.dptr = nullptr;
+  t.used_in = d.range_id;
   const uint32_t rows = (uint32_t)pow10u(L.Y.k);
   const hipError_t me = hipMalloc(&t.dptr, (size_t)rows * 64u * sizeof(uint32_t));
   if (me == hipErrorOutOfMemory) {
@@ -404,6 +412,7 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
 int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, bool profiling,
               uint64_t min_fast_threads, bool split, bool tabulate) {
   HIPCHK(hipSetDevice(d.ordinal));
+  d.range_id++;  // tables referenced from here on are pinned until the next call
   d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
   d.scan_launches = d.scan_nonces = d.scan_ops = 0;
   d.fast_ms = d.scan_ms = 0.0;
