@@ -269,6 +269,47 @@ def cpu_baseline(msg, start, target_s, runs=5):
     }
 
 
+def scaling_report(units, steps, ms_per_step):
+    """Per-GPU accounting of a timed run (one entry per rank under torchrun,
+    per device in library mode), so an N > 1 line explains its own scaling:
+    a straggler shard shows as kernel_ms_max_over_mean > 1, a slow exchange
+    as gather_ms_per_step, launch/host skew as step time not covered by the
+    slowest GPU's kernels.  Each unit: shard_lo/shard_hi (lo > hi: empty),
+    nonces, launches, alg_ops, kernel_ms, scan_ms, gather_ms (sums over the
+    timed steps)."""
+    out = []
+    for u in units:
+        k = u["kernel_ms"]
+        e = {"unit": u.get("rank", u.get("device")),
+             "shard": [u["shard_lo"], u["shard_hi"]] if u["shard_lo"] <= u["shard_hi"] else None,
+             "nonces_per_step": u["nonces"] / steps,
+             "launches_per_step": u["launches"] / steps,
+             "kernel_ms_per_step": k / steps,
+             "scan_ms_per_step": u["scan_ms"] / steps,
+             "gather_ms_per_step": u["gather_ms"] / steps,
+             "frac": (u["alg_ops"] / (k * 1e-3) / VALU_PEAK_OPS) if k > 0 else None,
+             "kernel_GH_s": (u["nonces"] / (k * 1e-3) / 1e9) if k > 0 else None}
+        if "ordinal" in u:
+            e["ordinal"] = u["ordinal"]
+        out.append(e)
+    ks = [e["kernel_ms_per_step"] for e in out if e["shard"] is not None]
+    rep = {"units": out}
+    if ks and max(ks) > 0:
+        mean = sum(ks) / len(ks)
+        slow = max(range(len(out)), key=lambda i: out[i]["kernel_ms_per_step"])
+        rep.update({
+            "kernel_ms_max_over_mean": max(ks) / mean,
+            "slowest_unit": out[slow]["unit"],
+            "slowest_kernel_ms_per_step": max(ks),
+            "gather_ms_per_step_max": max(e["gather_ms_per_step"] for e in out),
+            # ms_per_step = slowest kernel + everything else (planning, launch,
+            # sync, the all-gather, skew between GPUs)
+            "step_ms_not_in_slowest_kernel": ms_per_step - max(ks),
+            "kernel_share_of_step": max(ks) / ms_per_step if ms_per_step > 0 else None,
+        })
+    return rep
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -332,9 +373,12 @@ def main():
         sync_devs = devices
     init_ms = (time.perf_counter() - t_init) * 1e3
 
+    timing = {}  # torchrun: this rank's scan / all-gather time of the timed steps
+
     def step():
         if mode == "torchrun":
-            return distributed_scan(msg, 0, total - 1, p1_amd.scan, device=coll_dev, shard_fn=p1_amd.plan_shards)
+            return distributed_scan(msg, 0, total - 1, p1_amd.scan, device=coll_dev, shard_fn=p1_amd.plan_shards,
+                                    timing=timing)
         return p1_amd.scan(msg, 0, total - 1)  # library: shards + RCCL all-gather inside
 
     def barrier():
@@ -345,6 +389,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    timing.clear()
     p1_amd.reset_stats()
     p1_amd.set_profiling(True)
     barrier()
@@ -360,9 +405,27 @@ def main():
     stats = p1_amd.get_stats()
 
     if mode == "torchrun":
-        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        from p1_amd.dist import gather_rank_stats
+
+        shard = timing.get("shard")
+        units = gather_rank_stats({
+            "shard_lo": shard[0] if shard else 1, "shard_hi": shard[1] if shard else 0,
+            "nonces": stats["scan_nonces"], "launches": stats["scan_launches"], "alg_ops": stats["scan_alg_ops"],
+            "kernel_ms": stats["scan_kernel_ms"], "scan_ms": timing.get("scan_s", 0.0) * 1e3,
+            "gather_ms": timing.get("gather_s", 0.0) * 1e3, "elapsed_ms": elapsed * 1e3,
+            "step_ms_median": statistics.median(step_ms) if step_ms else 0.0}, device=coll_dev)
+        elapsed = max(u["elapsed_ms"] for u in units) / 1e3  # max over ranks
+    else:
+        units = []
+        for i in range(len(devices)):
+            ds = p1_amd.get_device_stats(i)
+            units.append({"device": i, "ordinal": ds["ordinal"],
+                          "shard_lo": ds["shard_first"], "shard_hi": ds["shard_last"] if ds["active"] else 0,
+                          "nonces": ds["scan_nonces"], "launches": ds["scan_launches"],
+                          "alg_ops": ds["scan_alg_ops"], "kernel_ms": ds["scan_kernel_ms"],
+                          "scan_ms": ds["phase1_ms"], "gather_ms": ds["gather_ms"]})
+            if not ds["active"]:
+                units[-1]["shard_lo"] = 1
 
     result = results[-1]
     consistent = all(r == result for r in results)
@@ -473,6 +536,7 @@ def main():
                 "devices": devices if mode != "torchrun" else f"one per rank, {world} ranks",
             },
             "roofline": roofline,
+            "per_gpu": scaling_report(units, args.steps, ms_per_step),
             "result": {"hash": result[0], "nonce": result[1], "consistent": consistent,
                        "matches_known": (tuple(result) == tuple(known)) if known else None},
         }

@@ -36,7 +36,9 @@ extern "C" {
 
 #define P1HIP_OK 0
 #define P1HIP_ERR_NO_DEVICE (-1) /* no gfx950 device visible / bad ordinal      */
-#define P1HIP_ERR_HIP (-2)       /* HIP runtime error                           */
+#define P1HIP_ERR_HIP (-2)       /* HIP runtime error, or a host-side failure
+                                    (allocation, thread creation): no C++
+                                    exception ever crosses this ABI            */
 #define P1HIP_ERR_RCCL (-3)      /* RCCL error (multi-device all-gather)        */
 #define P1HIP_ERR_ARGS (-4)      /* msg==NULL with msg_len>0, msg_len too large */
 
@@ -114,7 +116,31 @@ typedef struct {
                                 (recorded only while profiling is on)            */
   uint64_t small_scans;      /* device scans that took the one-launch small path
                                 (<= 2^16 nonces: k_scan_small, fused reduce)     */
+  uint64_t table_replans;    /* device shares re-planned without MODE 5 because a
+                                K+W table could not be had (before any launch)   */
 } p1hip_stats_t;
+
+/* Per-device accounting since p1hip_reset_stats (device `index` in the order
+ * p1hip_init / p1hip_init_devices opened them), so a multi-device scan can
+ * explain its own scaling: which shard each device took, how long its
+ * kernels ran, how long its host thread spent in the scan phase and in the
+ * all-gather phase. */
+typedef struct {
+  int32_t ordinal;           /* HIP device ordinal                                */
+  int32_t active;            /* its shard of the last scan was non-empty          */
+  uint64_t shard_first;      /* last scan's shard [first, last] (first > last:    */
+  uint64_t shard_last;       /*   empty)                                          */
+  uint64_t scans;            /* p1hip_scan calls this device took part in         */
+  uint64_t scan_launches;    /* k_scan / k_scan_small launches                    */
+  uint64_t scan_nonces;      /* nonces they hashed                                */
+  uint64_t scan_alg_ops;     /* their algorithmic int32 ops (1384 * B_tail each)  */
+  double scan_kernel_ms;     /* HIP-event kernel time (while profiling is on)     */
+  double phase1_ms;          /* host wall ms: plan + launches + stream sync       */
+  double gather_ms;          /* host wall ms in the RCCL all-gather phase (0 for  */
+                             /*   one device / host combine)                      */
+} p1hip_device_stats_t;
+
+int p1hip_get_device_stats(int index, p1hip_device_stats_t *out);
 
 /* Record HIP events (on the library's own stream) around every fast-kernel
  * launch.  Off by default: the events cost a little host time per launch. */

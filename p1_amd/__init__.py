@@ -19,6 +19,7 @@ from ._lib import (  # noqa: F401
     plan_shards,
     set_profiling,
     get_stats,
+    get_device_stats,
     reset_stats,
     device_count,
     shutdown,

@@ -33,6 +33,26 @@ class Stats(ctypes.Structure):
         ("scan_alg_ops", U64),
         ("scan_kernel_ms", ctypes.c_double),
         ("small_scans", U64),
+        ("table_replans", U64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class DeviceStats(ctypes.Structure):
+    _fields_ = [
+        ("ordinal", ctypes.c_int32),
+        ("active", ctypes.c_int32),
+        ("shard_first", U64),
+        ("shard_last", U64),
+        ("scans", U64),
+        ("scan_launches", U64),
+        ("scan_nonces", U64),
+        ("scan_alg_ops", U64),
+        ("scan_kernel_ms", ctypes.c_double),
+        ("phase1_ms", ctypes.c_double),
+        ("gather_ms", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -59,6 +79,7 @@ SIGNATURES = [
     ("p1hip_set_profiling", ctypes.c_int, [ctypes.c_int]),
     ("p1hip_get_stats", ctypes.c_int, [ctypes.POINTER(Stats)]),
     ("p1hip_reset_stats", None, []),
+    ("p1hip_get_device_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(DeviceStats)]),
     ("p1hip_device_count", ctypes.c_int, []),
     ("p1hip_last_error", ctypes.c_char_p, []),
     ("p1hip_version", ctypes.c_char_p, []),
@@ -148,6 +169,13 @@ def set_profiling(on):
 def get_stats():
     s = Stats()
     _check(load().p1hip_get_stats(ctypes.byref(s)))
+    return s.as_dict()
+
+
+def get_device_stats(index):
+    """Per-device accounting since reset_stats (p1hip_get_device_stats)."""
+    s = DeviceStats()
+    _check(load().p1hip_get_device_stats(int(index), ctypes.byref(s)))
     return s.as_dict()
 
 

@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <exception>
 #include <mutex>
@@ -57,6 +58,20 @@ int fail(int rc, const std::string& what) {
   return rc;
 }
 
+// Run an exported entry point's body; a host exception (std::bad_alloc from a
+// caller-sized allocation, std::system_error from a thread) becomes rc -2
+// with the message in p1hip_last_error() instead of crossing the C ABI.
+template <typename Fn>
+int guarded(Fn&& fn) {
+  try {
+    return fn();
+  } catch (const std::exception& ex) {
+    return fail(P1HIP_ERR_HIP, std::string("host: ") + ex.what());
+  } catch (...) {
+    return fail(P1HIP_ERR_HIP, "host: unknown exception");
+  }
+}
+
 #define HIPCHK(expr)                                                                        \
   do {                                                                                      \
     hipError_t e_ = (expr);                                                                 \
@@ -88,13 +103,14 @@ uint64_t small_limit() {
 }
 
 // P1HIP_MAX_LAUNCH_BLOCKS (tests only, read per scan): a lower per-launch
-// workgroup cap, so a full-size GPU test still runs the multi-launch path.
-// Never below one fast piece (kMaxFastThreads / kBlock workgroups).
+// workgroup cap, so GPU tests run the multi-launch path on small ranges.  A
+// piece larger than the cap gets a launch of its own (a piece is at most
+// kMaxFastThreads / kBlock = 2^18 workgroups, far below HIP's grid limit).
 uint64_t launch_block_limit() {
   const char* v = getenv("P1HIP_MAX_LAUNCH_BLOCKS");
   const uint64_t n = v && *v ? strtoull(v, nullptr, 10) : 0;
   if (n == 0 || n >= kMaxLaunchBlocks) return kMaxLaunchBlocks;
-  return n < kMaxFastThreads / kBlock ? kMaxFastThreads / kBlock : n;
+  return n;
 }
 
 struct Dev {
@@ -130,6 +146,9 @@ struct Dev {
   double fast_ms = 0.0;
   uint64_t scan_launches = 0, scan_nonces = 0, scan_ops = 0;
   double scan_ms = 0.0;
+  uint64_t replans = 0;         // shares re-planned without MODE 5 (this scan)
+  // since p1hip_reset_stats, for p1hip_get_device_stats
+  p1hip_device_stats_t acc{};
 };
 
 struct Runtime {
@@ -417,8 +436,29 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
   d.scan_launches = d.scan_nonces = d.scan_ops = 0;
   d.fast_ms = d.scan_ms = 0.0;
   Plan plan;
-  std::string err = make_plan(msg, len, lo, hi, plan, true, min_fast_threads, split, tabulate);
-  if (!err.empty()) return fail(P1HIP_ERR_ARGS, "planner: " + err);
+  // plan -> every MODE 5 table -> launches: a table that cannot be had makes
+  // the share re-plan without MODE 5 here, before any k_scan of it (or any
+  // segment-table copy) is enqueued, so nothing is scanned twice and no
+  // buffer is reallocated behind queued work.  Tables already built stay
+  // cached (their k_kwtable launches are complete work, not scan work).
+  std::vector<uint64_t> tabptr;
+  for (;;) {
+    std::string err = make_plan(msg, len, lo, hi, plan, true, min_fast_threads, split, tabulate);
+    if (!err.empty()) return fail(P1HIP_ERR_ARGS, "planner: " + err);
+    tabptr.assign(plan.launches.size(), 0);
+    bool replan = false;
+    for (size_t i = 0; i < plan.launches.size() && !replan; ++i) {
+      const Launch& L = plan.launches[i];
+      if (!L.fast || L.mode != 5) continue;
+      const int rt = kwtable_for(d, L, &tabptr[i]);
+      if (rt == kNoTable) replan = true;
+      else if (rt != P1HIP_OK) return rt;
+    }
+    if (!replan) break;
+    tabulate = false;  // the re-plan has no MODE 5 launch, so this loop ends
+    d.replans++;
+    plan = Plan();
+  }
   // Longest-running workgroups first: fast pieces by lo-loop length (10^k),
   // then generic pieces, so short work fills the grid's drain.
   std::vector<size_t> order(plan.launches.size());
@@ -487,12 +527,7 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
         if (!has_variant(L.fv, L.mode, L.trail)) return fail(P1HIP_ERR_ARGS, "no fast kernel variant");
         S.kind = variant_id(L.fv, L.mode, L.trail);
         S.fa = L.fa;
-        if (L.mode == 5) {
-          const int rt = kwtable_for(d, L, &S.fa.kwtab);
-          if (rt == kNoTable)  // nothing launched yet: plan the share again without MODE 5
-            return run_range(d, msg, len, lo, hi, profiling, min_fast_threads, split, false);
-          if (rt != P1HIP_OK) return rt;
-        }
+        if (L.mode == 5) S.fa.kwtab = tabptr[order[B.first + j]];
         d.fast_launches++;
         d.fast_nonces += L.nonces;
         d.fast_ops += L.nonces * kAlgOpsPerCompression * (uint64_t)L.btail;
@@ -579,6 +614,11 @@ Key finish_key(Key k) {
   return k;
 }
 
+int scan_locked(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t upper, uint64_t* out_hash,
+                uint64_t* out_nonce);
+int reduce_pairs_locked(const uint64_t* hashes, const uint64_t* nonces, size_t n, uint64_t* out_hash,
+                        uint64_t* out_nonce);
+
 }  // namespace
 
 // ----------------------------------------------------------------------------
@@ -587,25 +627,30 @@ Key finish_key(Key k) {
 extern "C" {
 
 int p1hip_init(int want_devices, int* got_devices) {
-  Runtime& R = rt();
-  std::lock_guard<std::mutex> g(R.mu);
-  int count = 0;
-  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
-    return fail(P1HIP_ERR_NO_DEVICE, "no HIP device visible");
-  int n = want_devices <= 0 ? count : want_devices;
-  if (n > count) return fail(P1HIP_ERR_NO_DEVICE, "asked for more devices than visible");
-  std::vector<int> ords;
-  for (int i = 0; i < n; ++i) ords.push_back(i);
-  int rc = init_locked(R, ords);
-  if (got_devices) *got_devices = rc == 0 ? (int)R.devs.size() : 0;
-  return rc;
+  if (got_devices) *got_devices = 0;
+  return guarded([&]() {
+    Runtime& R = rt();
+    std::lock_guard<std::mutex> g(R.mu);
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+      return fail(P1HIP_ERR_NO_DEVICE, "no HIP device visible");
+    int n = want_devices <= 0 ? count : want_devices;
+    if (n > count) return fail(P1HIP_ERR_NO_DEVICE, "asked for more devices than visible");
+    std::vector<int> ords;
+    for (int i = 0; i < n; ++i) ords.push_back(i);
+    int rc = init_locked(R, ords);
+    if (got_devices) *got_devices = rc == 0 ? (int)R.devs.size() : 0;
+    return rc;
+  });
 }
 
 int p1hip_init_devices(const int* ordinals, int n) {
   if (!ordinals || n <= 0) return fail(P1HIP_ERR_ARGS, "empty device list");
-  Runtime& R = rt();
-  std::lock_guard<std::mutex> g(R.mu);
-  return init_locked(R, std::vector<int>(ordinals, ordinals + n));
+  return guarded([&]() {
+    Runtime& R = rt();
+    std::lock_guard<std::mutex> g(R.mu);
+    return init_locked(R, std::vector<int>(ordinals, ordinals + n));
+  });
 }
 
 int p1hip_device_count(void) {
@@ -619,6 +664,15 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
   if (!out_hash || !out_nonce) return fail(P1HIP_ERR_ARGS, "null output pointer");
   if (!msg && msg_len > 0) return fail(P1HIP_ERR_ARGS, "msg == NULL with msg_len > 0");
   if (msg_len > P1HIP_MAX_MSG_LEN) return fail(P1HIP_ERR_ARGS, "msg_len exceeds P1HIP_MAX_MSG_LEN");
+  return guarded([&]() { return scan_locked(msg, msg_len, lower, upper, out_hash, out_nonce); });
+}
+
+}  // extern "C"
+
+namespace {
+
+int scan_locked(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t upper, uint64_t* out_hash,
+                uint64_t* out_nonce) {
   Runtime& R = rt();
   std::lock_guard<std::mutex> g(R.mu);
   const auto t0 = std::chrono::steady_clock::now();
@@ -641,8 +695,23 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
       if (nd == 1) {
         fn(0);
       } else {
+        // every thread is created before any of them runs `fn`: if one cannot
+        // start, none enters the scan or the collective (a peer blocked in
+        // ncclAllGather waiting for a thread that never started would hang)
+        std::atomic<int> go{0};  // 0 wait, 1 run, -1 abort
         std::vector<std::thread> th;
-        for (size_t i = 0; i < nd; ++i) th.emplace_back(fn, i);
+        try {
+          for (size_t i = 0; i < nd; ++i)
+            th.emplace_back([&, i]() {
+              while (go.load(std::memory_order_acquire) == 0) std::this_thread::yield();
+              if (go.load(std::memory_order_acquire) == 1) fn(i);
+            });
+        } catch (...) {
+          go.store(-1, std::memory_order_release);
+          for (auto& t : th) t.join();
+          throw;
+        }
+        go.store(1, std::memory_order_release);
         for (auto& t : th) t.join();
       }
     };
@@ -656,23 +725,27 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
     run_threads([&](size_t i) {
       Dev& d = R.devs[i];
       int r = P1HIP_OK;
+      const auto p0 = std::chrono::steady_clock::now();
       // per-scan accounting starts empty on every device (an inactive shard
       // must not re-report its previous scan)
       d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
       d.scan_launches = d.scan_nonces = d.scan_ops = 0;
       d.fast_ms = d.scan_ms = 0.0;
+      d.replans = 0;
       d.small_used = false;
+      d.acc.shard_first = slo[i];
+      d.acc.shard_last = shi[i];
+      d.acc.active = active[i];
+      // a host exception inside a device thread would end the process
+      // (std::terminate): it becomes this device's error instead
+      try {
       if ((int)i == R.fail_device) {
         r = fail(P1HIP_ERR_HIP, "injected failure (P1HIP_TEST_FAIL_DEVICE)");
       } else if (active[i] && shi[i] - slo[i] < small_max) {
         d.small_used = true;
         r = run_small(d, msg, msg_len, slo[i], shi[i], !coll && nd == 1, R.profiling);
       } else if (active[i]) {
-        try {
-          r = run_share(d, msg, msg_len, slo[i], shi[i], R);
-        } catch (const std::exception& ex) {  // host allocation: never let it cross the C ABI
-          r = fail(P1HIP_ERR_HIP, std::string("host: ") + ex.what());
-        }
+        r = run_share(d, msg, msg_len, slo[i], shi[i], R);
       } else {
         // empty shard: contribute the identity key (all ones)
         if (hipSetDevice(d.ordinal) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipSetDevice");
@@ -687,6 +760,10 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
           r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(result)");
       }
       if (!r && hipStreamSynchronize(d.stream) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipStreamSynchronize");
+      } catch (const std::exception& ex) {
+        r = fail(P1HIP_ERR_HIP, std::string("host: ") + ex.what());
+      }
+      d.acc.phase1_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - p0).count();
       rcs[i] = r;
       if (r) errs[i] = g_err;
     });
@@ -699,6 +776,7 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
       run_threads([&](size_t i) {
         Dev& d = R.devs[i];
         int r = P1HIP_OK;
+        const auto g0 = std::chrono::steady_clock::now();
         if (hipSetDevice(d.ordinal) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipSetDevice");
         if (!r) {
           ncclResult_t nr = ncclAllGather(d.d_res, d.d_gather, 2, ncclUint64, d.comm, d.stream);
@@ -708,6 +786,7 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
             hipMemcpyAsync(d.h_res, d.d_gather, sizeof(Key) * nd, hipMemcpyDeviceToHost, d.stream) != hipSuccess)
           r = fail(P1HIP_ERR_HIP, "hipMemcpyAsync(gathered)");
         if (!r && hipStreamSynchronize(d.stream) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipStreamSynchronize");
+        d.acc.gather_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g0).count();
         rcs[i] = r;
         if (r) errs[i] = g_err;
       });
@@ -728,6 +807,12 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
       R.stats.scan_alg_ops += d.scan_ops;
       R.stats.scan_kernel_ms += d.scan_ms;
       if (d.small_used && d.scan_launches) R.stats.small_scans++;
+      R.stats.table_replans += d.replans;
+      d.acc.scans++;
+      d.acc.scan_launches += d.scan_launches;
+      d.acc.scan_nonces += d.scan_nonces;
+      d.acc.scan_alg_ops += d.scan_ops;
+      d.acc.scan_kernel_ms += d.scan_ms;
     }
   }
   R.stats.scans++;
@@ -738,6 +823,10 @@ int p1hip_scan(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t uppe
   return P1HIP_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
 int p1hip_plan_shards(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t upper, int n,
                       uint64_t* first, uint64_t* last) {
   if (n <= 0 || !first || !last) return fail(P1HIP_ERR_ARGS, "n <= 0 or null output");
@@ -747,8 +836,10 @@ int p1hip_plan_shards(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64
     for (int i = 0; i < n; ++i) { first[i] = 1; last[i] = 0; }
     return P1HIP_OK;
   }
-  plan_shards(msg, msg_len, lower, upper, n, first, last);
-  return P1HIP_OK;
+  return guarded([&]() {
+    plan_shards(msg, msg_len, lower, upper, n, first, last);
+    return P1HIP_OK;
+  });
 }
 
 int p1hip_hash(const uint8_t* msg, size_t msg_len, uint64_t nonce, uint64_t* out_hash) {
@@ -759,6 +850,14 @@ int p1hip_hash(const uint8_t* msg, size_t msg_len, uint64_t nonce, uint64_t* out
 int p1hip_reduce_pairs(const uint64_t* hashes, const uint64_t* nonces, size_t n, uint64_t* out_hash,
                        uint64_t* out_nonce) {
   if (!out_hash || !out_nonce || (n && (!hashes || !nonces))) return fail(P1HIP_ERR_ARGS, "null pointer");
+  return guarded([&]() { return reduce_pairs_locked(hashes, nonces, n, out_hash, out_nonce); });
+}
+
+}  // extern "C"
+
+namespace {
+int reduce_pairs_locked(const uint64_t* hashes, const uint64_t* nonces, size_t n, uint64_t* out_hash,
+                        uint64_t* out_nonce) {
   Runtime& R = rt();
   std::lock_guard<std::mutex> g(R.mu);
   int rc = ensure_init(R);
@@ -797,6 +896,9 @@ int p1hip_reduce_pairs(const uint64_t* hashes, const uint64_t* nonces, size_t n,
   *out_nonce = res.n;
   return P1HIP_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int p1hip_set_profiling(int on) {
   Runtime& R = rt();
@@ -817,6 +919,20 @@ void p1hip_reset_stats(void) {
   Runtime& R = rt();
   std::lock_guard<std::mutex> g(R.mu);
   R.stats = p1hip_stats_t{};
+  for (Dev& d : R.devs) {
+    d.acc = p1hip_device_stats_t{};
+    d.acc.shard_first = 1;  // empty until the next scan
+  }
+}
+
+int p1hip_get_device_stats(int index, p1hip_device_stats_t* out) {
+  if (!out) return fail(P1HIP_ERR_ARGS, "null stats pointer");
+  Runtime& R = rt();
+  std::lock_guard<std::mutex> g(R.mu);
+  if (index < 0 || (size_t)index >= R.devs.size()) return fail(P1HIP_ERR_ARGS, "device index out of range");
+  *out = R.devs[(size_t)index].acc;
+  out->ordinal = R.devs[(size_t)index].ordinal;
+  return P1HIP_OK;
 }
 
 const char* p1hip_last_error(void) { return g_err.c_str(); }

@@ -97,7 +97,15 @@ void on_ack(Peer& p, int64_t seq, int window, const SendFn& send) {
 // A data message (Size already checked).  Every copy is acked -- the first
 // ack may have been lost; only new sequence numbers are kept, and delivery
 // is strictly in order (p1.pdf 2.1.2).
-void on_data(Peer& p, Message& m, const SendFn& send, const DeliverFn& deliver) {
+// A correct sender never has a message at or beyond expect + WindowSize in
+// flight (its window starts at its oldest un-acked message, which is at or
+// below our `expect`), so anything that far ahead comes from a faulty peer:
+// it is dropped un-acked, as if lost, which bounds `early` to
+// kEarlyWindows windows instead of letting a peer grow it without limit.
+constexpr int64_t kEarlyWindows = 4;
+void on_data(Peer& p, Message& m, int window, const SendFn& send, const DeliverFn& deliver) {
+  const int64_t ahead = kEarlyWindows * (window > 16 ? window : 16);
+  if (m.SeqNum >= p.expect + ahead) return;
   send(NewAck(p.conn_id, m.SeqNum));
   p.got_data = true;
   if (m.SeqNum < p.expect) return;
@@ -174,7 +182,11 @@ class Loop {
       pollfd pf[2] = {{conn_->fd(), POLLIN, 0}, {wake_, POLLIN, 0}};
       int rc = poll(pf, 2, timeout);
       if (stop_) break;
-      if (rc > 0 && (pf[0].revents & POLLIN)) {
+      // POLLERR without POLLIN: a pending ICMP error (e.g. port unreachable
+      // after the server died) on the connected client socket.  recvfrom
+      // consumes it (ECONNREFUSED below); left alone, poll would return at
+      // once on every iteration and spin until the next epoch's send.
+      if (rc > 0 && (pf[0].revents & (POLLIN | POLLERR))) {
         for (;;) {  // drain every queued datagram
           lspnet::UDPAddr from;
           ssize_t n = conn_->ReadFromUDP(buf.data(), buf.size(), &from);
@@ -297,7 +309,7 @@ class ClientImpl : public Client {
       on_ack(p_, m.SeqNum, prm_.WindowSize, send_);
       if (p_.out.empty()) cv_.notify_all();  // Close may be waiting
     } else if (m.Type == MsgData) {
-      on_data(p_, m, send_, [this](std::string&& s) { inbox_.push_back(std::move(s)); });
+      on_data(p_, m, prm_.WindowSize, send_, [this](std::string&& s) { inbox_.push_back(std::move(s)); });
       cv_.notify_all();
     }
   }
@@ -454,7 +466,7 @@ class ServerImpl : public Server {
     } else if (m.Type == MsgData) {
       const bool hide = c.closing;
       const int64_t id = c.p.conn_id;
-      on_data(c.p, m, send, [this, hide, id](std::string&& s) {
+      on_data(c.p, m, prm_.WindowSize, send, [this, hide, id](std::string&& s) {
         if (!hide) inbox_.push_back({id, std::move(s), false});
       });
       cv_.notify_all();

@@ -10,7 +10,11 @@
 //   :153-167  a Join makes a miner idle and hands it the oldest queued job
 // The handout (p1.pdf 4.2) asks the server to split large requests over the
 // miners, to schedule fairly and to survive miner and client loss.  Here:
-//   * a request [Lower, Upper] becomes chunks of at most `chunk` nonces;
+//   * a request [Lower, Upper] is carved into chunks of at most `chunk`
+//     nonces on demand: it holds only a cursor (next unsent nonce, Upper) and
+//     a short queue of chunks handed back by lost miners, so its memory is
+//     O(1) in the range size -- client.go:21 accepts any uint64 maxNonce and
+//     server.go:119-140 forwards any range, so [0, 2^64-1] must be cheap;
 //   * idle miners take chunks round-robin over the open requests, so a small
 //     request is not starved behind a large one;
 //   * a lost miner's chunk goes back to the front of its request's queue;
@@ -52,17 +56,13 @@ class Scheduler {
     r.id = next_id_++;
     r.client = client;
     r.data = data;
-    if (lo <= hi) {
-      for (uint64_t a = lo;;) {
-        const uint64_t b = (hi - a >= chunk_) ? a + (chunk_ - 1) : hi;
-        r.todo.push_back({a, b});
-        if (b == hi) break;
-        a = b + 1;
-      }
-    }
+    r.next = lo;
+    r.hi = hi;
+    r.exhausted = lo > hi;  // an empty range is answered at once (identity)
     order_.push_back(r.id);
     const uint64_t id = r.id;
     reqs_.emplace(id, std::move(r));
+    if (lo > hi) done_.push_back(id);
     return id;
   }
 
@@ -101,6 +101,7 @@ class Scheduler {
     if (r == reqs_.end()) return true;  // its client is gone
     Req& q = r->second;
     q.outstanding--;
+    if (!q.has_work() && q.outstanding == 0) done_.push_back(q.id);
     // a chunk whose hashes are all MaxUint64 reports (Max, 0); only real
     // minima (< Max) take part, lexicographically -- identity of miner.go:56
     if (hash < UINT64_MAX && (!q.found || hash < q.best || (hash == q.best && nonce < q.best_n))) {
@@ -121,10 +122,9 @@ class Scheduler {
       for (size_t tries = 0; tries < order_.size(); ++tries) {
         const uint64_t id = order_[rr_++ % order_.size()];
         auto it = reqs_.find(id);
-        if (it == reqs_.end() || it->second.todo.empty()) continue;
+        if (it == reqs_.end() || !it->second.has_work()) continue;
         Req& r = it->second;
-        const Span c = r.todo.front();
-        r.todo.pop_front();
+        const Span c = r.take(chunk_);
         r.outstanding++;
         m.busy = true;
         m.cur_req = id;
@@ -143,20 +143,26 @@ class Scheduler {
   // drop the miner.
   void Unassign(int miner) { LoseMiner(miner); }
 
-  // Requests whose chunks are all answered, in completion order.
+  // Requests whose chunks are all answered, in the order they completed.
   std::vector<Done> TakeDone() {
     std::vector<Done> out;
-    for (auto it = reqs_.begin(); it != reqs_.end();) {
-      Req& r = it->second;
-      if (r.todo.empty() && r.outstanding == 0) {
-        out.push_back({r.id, r.client, r.found ? r.best : UINT64_MAX, r.found ? r.best_n : 0});
-        drop_order(r.id);
-        it = reqs_.erase(it);
-      } else {
-        ++it;
-      }
+    for (uint64_t id : done_) {
+      auto it = reqs_.find(id);
+      if (it == reqs_.end()) continue;  // its client went away meanwhile
+      const Req& r = it->second;
+      out.push_back({r.id, r.client, r.found ? r.best : UINT64_MAX, r.found ? r.best_n : 0});
+      drop_order(r.id);
+      reqs_.erase(it);
     }
+    done_.clear();
     return out;
+  }
+
+  // Chunks a request still holds in memory (handed-back chunks; the unsent
+  // rest of its range is one cursor).  Tests bound this.
+  size_t HeldSpans(uint64_t req) const {
+    auto it = reqs_.find(req);
+    return it == reqs_.end() ? 0 : it->second.back.size();
   }
 
   bool Idle() const { return reqs_.empty(); }
@@ -171,10 +177,26 @@ class Scheduler {
     uint64_t id;
     int64_t client;
     std::string data;
-    std::deque<Span> todo;
+    std::deque<Span> back;       // chunks handed back by lost miners (sent first)
+    uint64_t next = 0, hi = 0;   // cursor: [next, hi] not handed out yet
+    bool exhausted = false;      // the cursor has passed hi
     uint64_t outstanding = 0;
     uint64_t best = UINT64_MAX, best_n = 0;
     bool found = false;
+    bool has_work() const { return !back.empty() || !exhausted; }
+    // next chunk: a handed-back one, else carved from the cursor
+    Span take(uint64_t chunk) {
+      if (!back.empty()) {
+        const Span c = back.front();
+        back.pop_front();
+        return c;
+      }
+      const uint64_t b = (hi - next >= chunk) ? next + (chunk - 1) : hi;
+      const Span c{next, b};
+      if (b == hi) exhausted = true;  // no wrap at 2^64-1
+      else next = b + 1;
+      return c;
+    }
   };
   struct Miner {
     bool busy = false;
@@ -185,7 +207,7 @@ class Scheduler {
     auto it = reqs_.find(req);
     if (it == reqs_.end()) return;
     it->second.outstanding--;
-    it->second.todo.push_front({lo, hi});
+    it->second.back.push_front({lo, hi});
   }
   void drop_order(uint64_t id) {
     for (size_t i = 0; i < order_.size(); ++i)
@@ -199,6 +221,7 @@ class Scheduler {
   std::map<int, Miner> miners_;
   std::map<uint64_t, Req> reqs_;
   std::vector<uint64_t> order_;
+  std::vector<uint64_t> done_;  // completed request ids, in completion order
   size_t rr_ = 0;
   uint64_t next_id_ = 1;
 };

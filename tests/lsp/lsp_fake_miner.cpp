@@ -5,6 +5,8 @@
 //   lsp_fake_miner <host:port> [--epoch-limit K] [--epoch-millis M] [--window W]
 // FAKE_DIE_AFTER=n: after answering n requests, read the next one and exit
 // without answering or closing (a miner the server must declare lost).
+// FAKE_LOG=path: append "lower upper" of every request received (tests check
+// what the server handed out).
 // P1LSP_* env vars inject loss (lspnet.hpp).
 #include <stdio.h>
 #include <stdlib.h>
@@ -33,6 +35,7 @@ int main(int argc, char** argv) {
   }
   const char* die = getenv("FAKE_DIE_AFTER");
   const long die_after = die && *die ? atol(die) : -1;
+  const char* logp = getenv("FAKE_LOG");
   std::string err;
   std::unique_ptr<lsp::Client> cli = lsp::NewClient(argv[1], prm, &err);
   if (!cli) {
@@ -47,6 +50,12 @@ int main(int argc, char** argv) {
     if (answered == die_after) _exit(3);  // vanish: no answer, no Close
     bitcoin::Message req;
     if (!bitcoin::Unmarshal(buf, &req)) req = bitcoin::Message();
+    if (logp && *logp) {
+      if (FILE* f = fopen(logp, "a")) {
+        fprintf(f, "%llu %llu\n", (unsigned long long)req.Lower, (unsigned long long)req.Upper);
+        fclose(f);
+      }
+    }
     uint64_t h = UINT64_MAX, n = 0;
     if (req.Lower <= req.Upper) p1o_scan((const uint8_t*)req.Data.data(), req.Data.size(), req.Lower, req.Upper, &h, &n);
     if (!cli->Write(bitcoin::Marshal(bitcoin::NewResult(h, n)))) break;

@@ -79,3 +79,22 @@ def test_dist_flag_rehearses_torchrun_path_at_world_one():
     r = bench.resolve_run(1, "c4", {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, visible=1, force_dist=True)
     assert r["mode"] == "torchrun" and r["n"] == 1 and r["world"] == 1
     assert bench.resolve_run(1, None, {}, visible=1)["mode"] == "single"  # the driver's N=1 launch
+
+
+def test_scaling_report_names_the_straggler():
+    # 4 GPUs, 10 steps: GPU 2 runs 10% longer kernels, GPU 3 had an empty shard
+    units = []
+    for i, k in enumerate([1000.0, 1000.0, 1100.0, 0.0]):
+        units.append({"rank": i, "shard_lo": 100 * i if k else 1, "shard_hi": 100 * i + 99 if k else 0,
+                      "nonces": 10 * (1 << 30) if k else 0, "launches": 10 if k else 0,
+                      "alg_ops": 10 * (1 << 30) * 1384 if k else 0, "kernel_ms": k, "scan_ms": k + 5.0,
+                      "gather_ms": 0.5})
+    rep = bench.scaling_report(units, steps=10, ms_per_step=112.0)
+    assert rep["slowest_unit"] == 2
+    assert abs(rep["kernel_ms_max_over_mean"] - 110.0 / (310.0 / 3)) < 1e-9
+    assert abs(rep["step_ms_not_in_slowest_kernel"] - 2.0) < 1e-9
+    assert rep["units"][3]["shard"] is None and rep["units"][3]["frac"] is None
+    assert rep["units"][0]["shard"] == [0, 99] and rep["units"][0]["nonces_per_step"] == 1 << 30
+    want_frac = (1 << 30) * 1384 / 0.1 / bench.VALU_PEAK_OPS
+    assert abs(rep["units"][0]["frac"] - want_frac) < 1e-12
+    assert rep["gather_ms_per_step_max"] == 0.05

@@ -68,3 +68,55 @@ def test_distributed_scan_gloo(world, planned, oracle_mod):
         exp = [plan_shards(m, lo, hi, world)[rank] if planned else shard_range(lo, hi, rank, world)
                for m, lo, hi in cases]
         assert calls == [e for e in exp if e is not None]
+
+
+def _stats_worker(rank, world, port, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    import oracle
+    from p1_amd.dist import distributed_scan, gather_rank_stats
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    timing = {}
+    for _ in range(3):
+        distributed_scan(b"bradfitz", 0, 9999, oracle.scan, timing=timing)
+    mine = {"shard_lo": timing["shard"][0], "shard_hi": (1 << 64) - 1 - rank, "nonces": rank + 1,
+            "launches": 2 * rank, "alg_ops": (1 << 63) + rank, "kernel_ms": 1.5 * rank,
+            "scan_ms": timing["scan_s"] * 1e3, "gather_ms": timing["gather_s"] * 1e3, "elapsed_ms": 10.0 + rank,
+            "step_ms_median": 3.25}
+    got = gather_rank_stats(mine)
+    dist.destroy_process_group()
+    q.put((rank, timing["steps"], timing["shard"], got))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_rank_stats_gloo(world):
+    """bench.py's N>1 diagnostics: every rank's shard, kernel and collective
+    time reach rank 0 intact (u64 values above 2^63 included)."""
+    from p1_amd import shard_range
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stats_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, steps, shard, got in res:
+        assert steps == 3 and tuple(shard) == shard_range(0, 9999, rank, world)
+        assert len(got) == world
+        for r, g in enumerate(got):
+            assert g["rank"] == r
+            assert g["shard_lo"] == shard_range(0, 9999, r, world)[0]
+            assert g["shard_hi"] == (1 << 64) - 1 - r and g["alg_ops"] == (1 << 63) + r
+            assert g["nonces"] == r + 1 and g["launches"] == 2 * r
+            assert g["kernel_ms"] == 1.5 * r and g["elapsed_ms"] == 10.0 + r and g["step_ms_median"] == 3.25
+            assert g["gather_ms"] >= 0.0 and g["scan_ms"] > 0.0

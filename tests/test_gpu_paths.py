@@ -125,6 +125,66 @@ def test_mode5_table_unavailable_replans(gpu, oracle_mod, monkeypatch):
         assert lo <= n <= hi and oracle_mod.hash(mm, n) == h
 
 
+def test_mode5_whole_blocks_vs_oracle(reinit, oracle_mod):
+    """MODE 5 with k = 1..7 digits in tail block 1, exactly against the
+    oracle over ranges holding whole 10^k-aligned blocks (VERDICT r02 #1:
+    k = 6, 7 had only been cross-checked GPU against GPU).  Occupancy floor 1
+    keeps the planner from lowering k, so the blocks really run MODE 5."""
+    g = reinit(P1HIP_MIN_FAST_THREADS=1)
+    rnd = random.Random(35)
+    g.reset_stats()
+    n_all = 0
+    for k in (1, 2, 3, 4, 5, 6, 7):
+        for r in (57, 50):  # (L + 1) % 64; 57 is configs[2]'s 120-byte message
+            d = k + 64 - r
+            if d > 20:
+                continue
+            L = r - 1 + (64 if r == 57 else 0)
+            m = b"cmu440-p1-" * 12 if L == 120 else bytes(rnd.randrange(32, 127) for _ in range(L))
+            blk = 10**k
+            base = 10 ** (d - 1) + rnd.randrange(1, 50) * blk
+            lo, hi = base - 777, base + 2 * blk + 555  # two whole blocks + ragged edges
+            assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=16), (k, r, lo, hi)
+            n_all += hi - lo + 1
+    s = g.get_stats()
+    assert s["table_replans"] == 0 and s["scan_nonces"] == n_all
+    assert s["fast_nonces"] > 0.9 * n_all  # the whole blocks ran in fast (MODE 5) segments
+
+
+def test_mode5_replan_before_any_launch(reinit, oracle_mod, monkeypatch):
+    """a MODE 5 table that cannot be had is found in a
+    pre-pass, before any k_scan of the share is enqueued.  The MODE 5 piece
+    (k = 1, weight 20) sorts behind a k = 3 TRAIL piece, so under a small
+    per-launch cap it lands in launch >= 2 -- where the old code re-planned
+    after launch 1 was already queued.  Now: the answer is the oracle's, one
+    re-plan is counted, every nonce is scanned once, and the launches are
+    exactly those of the same scan planned without MODE 5 at all."""
+    m = bytes(range(65, 65 + 53))  # L = 53: r = 54, d = 10 TRAIL (k = 3), d = 11 MODE 5 with k = 1
+    lo, hi = 10**10 - 10**8, 10**10 + 10**7
+    want = oracle_mod.scan(m, lo, hi, threads=16)
+    monkeypatch.setenv("P1HIP_MAX_LAUNCH_BLOCKS", "200")
+    g = reinit(P1HIP_MIN_FAST_THREADS=1, P1HIP_NO_TABLE=1)
+    g.reset_stats()
+    assert g.scan(m, lo, hi) == want
+    no_table = g.get_stats()
+    monkeypatch.delenv("P1HIP_NO_TABLE")
+    g = reinit(P1HIP_MIN_FAST_THREADS=1)
+    g.reset_stats()
+    assert g.scan(m, lo, hi) == want  # MODE 5 with its table
+    s = g.get_stats()
+    assert s["table_replans"] == 0 and s["scan_launches"] >= 2
+    monkeypatch.setenv("P1HIP_KWTAB_MAX_BYTES", "1000")  # even k = 1's 2.5 KB table is refused
+    g = reinit(P1HIP_MIN_FAST_THREADS=1)
+    g.reset_stats()
+    assert g.scan(m, lo, hi) == want
+    s = g.get_stats()
+    assert s["table_replans"] == 1
+    assert s["scan_nonces"] == hi - lo + 1
+    assert s["scan_launches"] == no_table["scan_launches"] >= 2
+    monkeypatch.delenv("P1HIP_KWTAB_MAX_BYTES")
+    monkeypatch.delenv("P1HIP_MAX_LAUNCH_BLOCKS")
+
+
 def test_rccl_allgather_one_device(reinit, oracle_mod):
     g = reinit(P1HIP_FORCE_RCCL=1)
     for m, lo, hi in [(b"bradfitz", 0, 9999), (b"msg", 0, 2), (b"msg", 7, 3), (b"x" * 70, 10**9 - 3000, 10**9 + 3000)]:

@@ -21,6 +21,25 @@ MINER = os.path.join(ROOT, "p1_amd", "p1miner")
 FAKE = os.path.join(ROOT, "tools", "lsp_fake_miner")
 
 
+def kfd_queues(pid):
+    """{queue type: count} of a process's user-mode queues from
+    /sys/class/kfd/kfd/proc/<pid>/queues/<id>/type, or None if not exposed."""
+    base = f"/sys/class/kfd/kfd/proc/{pid}/queues"
+    try:
+        ids = os.listdir(base)
+    except OSError:
+        return None
+    out = {}
+    for q in ids:
+        try:
+            with open(os.path.join(base, q, "type")) as f:
+                t = f.read().strip().lower()
+        except OSError:
+            t = "unreadable"
+        out[t] = out.get(t, 0) + 1
+    return out
+
+
 class System:
     """One server + miners; every process is ours and is killed by PID."""
 
@@ -125,6 +144,32 @@ def test_lost_miner_chunk_is_reassigned(system, oracle_mod):
     assert r.stdout.strip() == f"Result {h} {n}", r.stdout + r.stderr
 
 
+def test_full_u64_request_is_carved_on_demand(system, tmp_path):
+    """client.go:21 takes any uint64 maxNonce and server.go:119-140 forwards
+    any range: `p1client host msg 18446744073709551615` must be accepted and
+    its first chunks handed out at once, with the server's memory O(1) in the
+    range (an eager chunk list would need 1.8e16 spans here)."""
+    log = tmp_path / "chunks.txt"
+    s = system(["--chunk", "1000"])
+    s.miner(fake(), env={"FAKE_LOG": str(log)})
+    c = subprocess.Popen([CLIENT, s.hostport, "bradfitz", str((1 << 64) - 1)], stdout=subprocess.DEVNULL)
+    try:
+        deadline = time.time() + 30
+        lines = []
+        while time.time() < deadline:
+            lines = log.read_text().split("\n") if log.exists() else []
+            if len(lines) > 5:
+                break
+            time.sleep(0.1)
+        got = [tuple(map(int, x.split())) for x in lines if x.strip()]
+        assert got[:3] == [(0, 999), (1000, 1999), (2000, 2999)], got[:5]
+        rss_kb = int([x for x in open(f"/proc/{s.server.pid}/status") if x.startswith("VmRSS")][0].split()[1])
+        assert rss_kb < 64 * 1024, rss_kb
+    finally:
+        c.kill()
+        c.wait()
+
+
 def test_lost_client_does_not_block_others(system, oracle_mod):
     prm = ["--epoch-millis", "100", "--epoch-limit", "5"]
     s = system(["--chunk", "1000"] + prm)
@@ -182,6 +227,15 @@ def test_config5_over_lsp_8_gpu_miners_window8_drop5(system, oracle_mod):
     word, h, n = r.stdout.split()
     h, n = int(h), int(n)
     assert word == "Result" and oracle_mod.hash("bradfitz", n) == h
+    # Each miner has scanned; while it idles, count its hardware queues (KFD
+    # sysfs, when the box exposes it).  The r02i hang came from a second,
+    # null-stream queue per miner; one stream per process means one compute
+    # queue (DESIGN.md "Small scans").
+    queues = {p.pid: kfd_queues(p.pid) for p in s.procs[1:]}
+    print(f"configs[4] miner hardware queues (KFD sysfs): {queues}")
+    seen = [q for q in queues.values() if q is not None]
+    for q in seen:
+        assert q.get("compute", 0) <= 1, queues
     import p1_amd
 
     p1_amd.init_devices([0])
@@ -189,3 +243,74 @@ def test_config5_over_lsp_8_gpu_miners_window8_drop5(system, oracle_mod):
     b = p1_amd.scan("bradfitz", 1 << 35, hi)
     assert min(a, b) == (h, n)
     print(f"configs[4] over LSP: 2^36 nonces, 8 GPU miners, window 8, 5% drop: {wall:.2f} s wall")
+
+
+def _udp_frames(sock, seconds):
+    import json as _json
+    import socket as _socket
+
+    out, end = [], time.time() + seconds
+    while time.time() < end:
+        sock.settimeout(max(0.01, end - time.time()))
+        try:
+            out.append(_json.loads(sock.recv(2000)))
+        except (_socket.timeout, OSError):
+            break
+    return out
+
+
+def test_far_ahead_data_is_dropped_unacked(system):
+    """a peer's data far beyond the window (SeqNum >= expect +
+    4 x max(window, 16)) is dropped without an ack instead of being buffered
+    without bound; in-window data is acked and delivered in order."""
+    import base64
+    import json as _json
+    import socket as _socket
+
+    s = system(["--epoch-millis", "2000"])
+    sock = _socket.socket(_socket.AF_INET, _socket.SOCK_DGRAM)
+    sock.connect(("127.0.0.1", s.port))
+    sock.send(b'{"Type":0,"ConnID":0,"SeqNum":0,"Size":0,"Payload":null}')
+    ack = _udp_frames(sock, 1.0)[0]
+    assert ack["Type"] == 2 and ack["SeqNum"] == 0
+    cid = ack["ConnID"]
+    join = b'{"Type":0,"Data":"","Lower":0,"Upper":0,"Hash":0,"Nonce":0}'
+
+    def data(seq):
+        return _json.dumps({"Type": 1, "ConnID": cid, "SeqNum": seq, "Size": len(join),
+                            "Payload": base64.b64encode(join).decode()}).encode()
+
+    sock.send(data(1 + 64))  # expect is 1: 64 ahead = the bound for window 1
+    acks = [f["SeqNum"] for f in _udp_frames(sock, 0.5) if f["Type"] == 2]
+    assert 65 not in acks
+    sock.send(data(2))  # one ahead: buffered and acked
+    sock.send(data(1))
+    acks = [f["SeqNum"] for f in _udp_frames(sock, 0.5) if f["Type"] == 2]
+    assert 2 in acks and 1 in acks
+    sock.close()
+
+
+def test_client_does_not_spin_after_server_dies(system):
+    """an ICMP port-unreachable on the client's connected socket
+    raises POLLERR without POLLIN; the event loop must consume it, not spin
+    at 100% CPU until the epoch limit declares the connection lost."""
+    s = system(["--epoch-millis", "1000"])
+    p = subprocess.Popen([CLIENT, s.hostport, "bradfitz", "9999", "--epoch-millis", "1000", "--epoch-limit", "8"],
+                         stdout=subprocess.DEVNULL)
+    try:
+        time.sleep(0.5)
+        s.server.kill()
+        s.server.wait()
+        time.sleep(1.2)  # an epoch send hits the closed port: ICMP error pending
+
+        def cpu_s():
+            f = open(f"/proc/{p.pid}/stat").read().rsplit(")", 1)[1].split()
+            return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
+
+        c0, t0 = cpu_s(), time.time()
+        time.sleep(2.0)
+        used = (cpu_s() - c0) / (time.time() - t0)
+        assert used < 0.3, f"client used {used:.0%} of a core while its server was gone"
+    finally:
+        p.kill()
+        p.wait()

@@ -65,6 +65,18 @@ def test_serve_many_requests_in_order(oracle_mod):
     assert all(g["Type"] == 2 for g in got)
 
 
+def test_scheduler_unit(tmp_path):
+    """scheduler.hpp on its own: the full u64 range as one cursor, lost-miner
+    chunks first, identity and tie-breaking, completion order, cancelled
+    clients (tests/sched_test.cpp)."""
+    exe = str(tmp_path / "sched_test")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-o", exe,
+                    os.path.join(ROOT, "tests", "sched_test.cpp")], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "sched_test: ok"
+
+
 def test_usage():
     assert server([]).returncode == 2
     assert server(["--chunk", "0", "scan", "a", "0", "1"]).returncode == 2
