@@ -24,6 +24,17 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def large(golden):
+    """Exact full-range answers of the BASELINE configs, (msg bytes, lower,
+    upper) -> (hash, nonce): configs[1] from the survey's hashlib run,
+    configs[2]/[3]/[4] from tools/pin_large.c (a container-only SHA-NI /
+    AVX-512 restatement validated against the oracle and hashlib,
+    tests/golden/pin_large_validation.json)."""
+    return {(bytes.fromhex(v["msg_hex"]), v["lower"], v["upper"]): (v["hash"], v["nonce"])
+            for v in golden["scan"] if v.get("large")}
+
+
+@pytest.fixture(scope="session")
 def oracle_mod():
     import oracle
 

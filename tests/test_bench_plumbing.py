@@ -55,7 +55,18 @@ def test_job_sizes():
     assert bench.job_total(bench.CONFIGS["c4"], 8) == 1 << 38  # strong scaling: fixed job
     assert bench.job_total(bench.CONFIGS["c2"], 8) == 8 << 32  # weak scaling
     assert bench.known_answer(bench.CONFIGS["c4"], 8) == bench.known_answer(bench.CONFIGS["c4"], 1)
-    assert bench.known_answer(bench.CONFIGS["c2"], 1) == (5256245051, 1626825724)
+    assert bench.known_answer(bench.CONFIGS["c2"], 1)[0] == (5256245051, 1626825724)
+
+
+def test_known_answers_are_independent_pins():
+    # every bench workload at N = 1 (and c4 at any N) checks an answer that
+    # did not come from the GPU: hashlib (c2) or tools/pin_large.c (c3, c4)
+    c2, src2 = bench.known_answer(bench.CONFIGS["c2"], 1)
+    c3, src3 = bench.known_answer(bench.CONFIGS["c3"], 1)
+    c4, src4 = bench.known_answer(bench.CONFIGS["c4"], 8)
+    assert "hashlib" in src2 and "pin_large" in src3 and "pin_large" in src4
+    assert c3 == (1902263685, 2962726851) and c4 == (52863133, 182986939864)
+    assert bench.known_answer(bench.CONFIGS["c2"], 2) == (None, None)  # [0, 2^33): not pinned
 
 
 def test_cli_refuses_more_gpus_than_visible():

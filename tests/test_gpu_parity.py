@@ -101,13 +101,15 @@ def test_tie_breaking_reduction(gpu):
     assert gpu.reduce_pairs([U64_MAX, U64_MAX - 1], [1, 99]) == (U64_MAX - 1, 99)
 
 
-def test_full_size_properties_config3(gpu, oracle_mod):
-    """configs[2] (120-byte msg, [0, 2^34)) is too big for the CPU oracle, so
-    check size-independent properties: the reported nonce re-hashes to the
-    reported hash, and the scan is the min of its two halves (split at an
-    arbitrary point), each of which also re-hashes."""
+def test_full_size_config3_exact(gpu, oracle_mod, large):
+    """configs[2] (120-byte msg, [0, 2^34)): equal to the exact answer pinned
+    by tools/pin_large.c (independent CPU restatement, tests/golden), plus the
+    size-independent properties: the reported nonce re-hashes to the reported
+    hash, and the scan is the min of its two halves (split at an arbitrary
+    point), each of which also re-hashes."""
     hi = (1 << 34) - 1
     h, n = gpu.scan(M120, 0, hi)
+    assert (h, n) == large[(M120, 0, hi)]
     assert 0 <= n <= hi and oracle_mod.hash(M120, n) == h
     cut = 9_876_543_210
     a = gpu.scan(M120, 0, cut)
@@ -194,15 +196,17 @@ def test_reduce_pairs_large(gpu):
     assert gpu.reduce_pairs(hs, ns) == want
 
 
-def test_config4_range_on_one_gpu_multi_batch(gpu, oracle_mod, monkeypatch):
+def test_config4_range_on_one_gpu_multi_batch(gpu, oracle_mod, monkeypatch, large):
     """configs[3]'s whole [0, 2^38) on one GPU (~1.07M workgroups): one
     launch by default, and several launches (batches) under a 2^19-workgroup
-    cap (test knob P1HIP_MAX_LAUNCH_BLOCKS, read per scan).  Checked by
-    size-independent properties: both agree, the result re-hashes on the
-    oracle and equals the min of two independently scanned halves."""
+    cap (test knob P1HIP_MAX_LAUNCH_BLOCKS, read per scan).  Both equal the
+    exact answer pinned by tools/pin_large.c; also the size-independent
+    properties: the result re-hashes on the oracle and equals the min of two
+    independently scanned halves."""
     hi = (1 << 38) - 1
     gpu.reset_stats()
     h, n = gpu.scan("bradfitz", 0, hi)
+    assert (h, n) == large[(b"bradfitz", 0, hi)]
     assert gpu.get_stats()["scan_launches"] == 1
     assert oracle_mod.hash("bradfitz", n) == h
     monkeypatch.setenv("P1HIP_MAX_LAUNCH_BLOCKS", str(1 << 19))

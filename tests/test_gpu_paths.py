@@ -208,12 +208,13 @@ def test_failure_on_one_device_does_not_hang(reinit, oracle_mod):
     assert g.scan("bradfitz", 0, 9999) == (1419516646206828, 9898)
 
 
-def test_config5_full_size_split_over_8_miner_processes(gpu, oracle_mod):
+def test_config5_full_size_split_over_8_miner_processes(gpu, oracle_mod, large):
     """configs[4]'s job -- [0, 2^36) split by the server into 2^32-nonce
-    chunks over 8 GPU miner processes (here all on GPU 0) -- checked by
-    size-independent properties: the reported nonce re-hashes to the
-    reported hash on the oracle, and the result equals the min of two
-    independently scanned halves."""
+    chunks over 8 GPU miner processes (here all on GPU 0) -- equal to the
+    exact answer pinned by tools/pin_large.c, and by the size-independent
+    properties: the reported nonce re-hashes to the reported hash on the
+    oracle, and the result equals the min of two independently scanned
+    halves."""
     server = os.path.join(ROOT, "p1_amd", "p1server")
     hi = (1 << 36) - 1
     t0 = time.time()
@@ -224,8 +225,40 @@ def test_config5_full_size_split_over_8_miner_processes(gpu, oracle_mod):
     word, h, n = r.stdout.split()
     h, n = int(h), int(n)
     assert word == "Result"
+    assert (h, n) == large[(b"bradfitz", 0, hi)]
     assert oracle_mod.hash("bradfitz", n) == h
     a = gpu.scan("bradfitz", 0, (1 << 35) - 1)
     b = gpu.scan("bradfitz", 1 << 35, hi)
     assert min(a, b) == (h, n)
     print(f"configs[4] over stdio: 2^36 nonces, 8 miners on one GPU, {wall:.2f} s wall")
+
+
+def _hw_queues(argv, env=None):
+    """Distinct hardware queues the HIP runtime reports creating for one
+    process (its own log at AMD_LOG_LEVEL=3: "Created SWq=.. to map on HWq=..")."""
+    import re
+
+    e = dict(os.environ, AMD_LOG_LEVEL="3", **(env or {}))
+    r = subprocess.run(argv, capture_output=True, text=True, env=e, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    log = r.stdout + r.stderr
+    return set(re.findall(r"to map on HWq=(0x[0-9a-fA-F]+)", log)), log.count("Created SWq=")
+
+
+def test_one_hardware_queue_per_process():
+    """VERDICT r02 #4 / DESIGN "Small scans": the configs[4] hang of r02i was
+    put down to a second hardware queue per miner, created by a null-stream
+    hipMemset at init.  Measured here from the runtime's own log: a miner
+    process (`p1miner scan`) and the library alone create exactly one
+    hardware queue; the same program with one null-stream call added
+    (tools/queue_ctl nullstream, the control) creates two."""
+    miner = os.path.join(ROOT, "p1_amd", "p1miner")
+    ctl = os.path.join(ROOT, "tools", "queue_ctl")
+    q_miner, n_miner = _hw_queues([miner, "scan", "bradfitz", "0", str(10**8)])
+    q_lib, _ = _hw_queues([ctl])
+    q_null, n_null = _hw_queues([ctl, "nullstream"])
+    print(f"hardware queues: p1miner scan {len(q_miner)} ({n_miner} SWq), library {len(q_lib)}, "
+          f"with one null-stream call {len(q_null)} ({n_null} SWq)")
+    assert n_null >= 1, "the runtime log format changed: no queue creation lines"
+    assert len(q_miner) == 1 and len(q_lib) == 1
+    assert len(q_null) == 2

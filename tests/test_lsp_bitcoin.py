@@ -208,11 +208,12 @@ def test_bad_arguments():
 
 
 @pytest.mark.gpu
-def test_config5_over_lsp_8_gpu_miners_window8_drop5(system, oracle_mod):
+def test_config5_over_lsp_8_gpu_miners_window8_drop5(system, oracle_mod, large):
     """configs[4]: the server splits [0, 2^36) into 2^32-nonce chunks over 8
     GPU miner processes (all on GPU 0 here), LSP window 8, 5% of every write
-    dropped in every process.  Checked by size-independent properties: the
-    nonce re-hashes to the hash on the oracle and equals the min of two
+    dropped in every process.  Equal to the exact answer pinned by
+    tools/pin_large.c; also the size-independent properties: the nonce
+    re-hashes to the hash on the oracle and equals the min of two
     independently scanned halves (through the library, one GPU)."""
     env = {"P1LSP_WRITE_DROP": "5"}
     prm = ["--window", "8"]
@@ -227,6 +228,7 @@ def test_config5_over_lsp_8_gpu_miners_window8_drop5(system, oracle_mod):
     word, h, n = r.stdout.split()
     h, n = int(h), int(n)
     assert word == "Result" and oracle_mod.hash("bradfitz", n) == h
+    assert (h, n) == large[(b"bradfitz", 0, hi)]
     # Each miner has scanned; while it idles, count its hardware queues (KFD
     # sysfs, when the box exposes it).  The r02i hang came from a second,
     # null-stream queue per miner; one stream per process means one compute

@@ -4,7 +4,7 @@ configs[3], from tools/pin_large.c (an x86 SHA-NI / AVX-512 restatement of
 hash.go:13-17 + miner.go:56-63; test infrastructure, never the product).
 
   python tools/pin_large.py validate        # prove the tool first (see below)
-  python tools/pin_large.py pin c3|c4       # run it; record the answer in tests/golden/golden.json
+  python tools/pin_large.py pin c3|c4|c5    # run it; record the answer in tests/golden/golden.json
 
 `validate` requires pin_large == oracle/p1_oracle.c == hashlib on:
   * every scan and hash vector of tests/golden/golden.json (both of the tool's
@@ -34,6 +34,7 @@ M120 = b"cmu440-p1-" * 12
 JOBS = {
     "c3": (M120, 0, (1 << 34) - 1, "configs[2]: 120-byte msg, [0, 2^34)"),
     "c4": (b"bradfitz", 0, (1 << 38) - 1, "configs[3]: 'bradfitz', [0, 2^38)"),
+    "c5": (b"bradfitz", 0, (1 << 36) - 1, "configs[4]: 'bradfitz', [0, 2^36) (the LSP job over 8 GPU miners)"),
 }
 
 
