@@ -47,7 +47,10 @@ cd /tmp && export TMPDIR=/tmp
 for cfg in ${PROF_CONFIGS:-c2}; do
   pargs="--steps 1 --warmup 0 --no-cpu --no-small-request --config $cfg"
   if [ "${SKIP_PROF:-0}" != 1 ]; then
-    step rocprof_stats_$cfg 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_${cfg}_prof" -o run --output-format csv -- python3 "$ROOT/bench.py" $pargs
+    # the kernel trace of a bench run shaped like the timed one (warm-up
+    # steps, then timed steps): summarize_prof --skip-launches 2 averages the
+    # same launches bench.py's HIP events time
+    step rocprof_stats_$cfg 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_${cfg}_prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps ${PROF_STEPS:-3} --warmup 2 --no-cpu --no-small-request --config $cfg > "$OUT/${TAG}_${cfg}_prof_bench.json"
   fi
   if [ "${SKIP_PMC:-0}" != 1 ]; then
     i=0

@@ -22,20 +22,28 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def workload_stats(trace, out):
+def workload_stats(trace, out, skip=0):
     """rocprofv3 --kernel-trace rows of the workload's k_scan launches only
     (largest grid; bench.py's configs[0]-sized latency probe launches small
-    grids of the same kernel), in the --stats CSV layout."""
+    grids of the same kernel), in the --stats CSV layout.  With skip > 0 a
+    second row covers the launches after the first `skip` (the profiled
+    bench command's warm-up steps), i.e. the same launches bench.py's own
+    HIP events time."""
     rows = [r for r in csv.DictReader(open(trace)) if r["Kernel_Name"].split("(")[0] == "k_scan"]
     if not rows:
         return
     g = max(int(r["Grid_Size_X"]) for r in rows)
-    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if int(r["Grid_Size_X"]) == g]
-    mean = sum(d) / len(d)
-    sd = (sum((x - mean) ** 2 for x in d) / len(d)) ** 0.5
+    rows = sorted((r for r in rows if int(r["Grid_Size_X"]) == g), key=lambda r: int(r["Start_Timestamp"]))
+    d_all = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
     with open(out, "w") as f:
         f.write('"Name","Calls","TotalDurationNs","AverageNs","MinNs","MaxNs","StdDev","Grid_Size_X","Source"\n')
-        f.write(f'"k_scan",{len(d)},{sum(d)},{mean:.1f},{min(d)},{max(d)},{sd:.1f},{g},"{os.path.basename(trace)}"\n')
+        for name, d in (("k_scan", d_all), (f"k_scan (launches after the first {skip}: timed steps)", d_all[skip:])):
+            if not d or (name != "k_scan" and skip == 0):
+                continue
+            mean = sum(d) / len(d)
+            sd = (sum((x - mean) ** 2 for x in d) / len(d)) ** 0.5
+            f.write(f'"{name}",{len(d)},{sum(d)},{mean:.1f},{min(d)},{max(d)},{sd:.1f},{g},'
+                    f'"{os.path.basename(trace)}"\n')
 
 
 # Measured issue cost (SIMD cycles per wave instruction at 4 waves/SIMD,
@@ -53,6 +61,8 @@ def main():
     ap.add_argument("nonces_per_launch", nargs="?", type=float, default=2.0**32)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--nonces-total", type=float, default=None)
+    ap.add_argument("--skip-launches", type=int, default=0,
+                    help="warm-up launches of the profiled command (second row of the workload stats)")
     ap.add_argument("--half-rate-share", type=float, default=None,
                     help="share of class-A (half-rate) instructions in the executed loop mix")
     a = ap.parse_args()
@@ -65,7 +75,7 @@ def main():
         shutil.copy(ks, os.path.join(dst, f"{tag}_kernel_stats.csv"))
     kt = os.path.join(src, f"{tag}_prof", "run_kernel_trace.csv")
     if os.path.exists(kt):
-        workload_stats(kt, os.path.join(dst, f"{tag}_kernel_stats_workload.csv"))
+        workload_stats(kt, os.path.join(dst, f"{tag}_kernel_stats_workload.csv"), a.skip_launches)
     for f in glob.glob(os.path.join(src, f"{tag}_bench*.json")) + glob.glob(os.path.join(src, f"{tag}_valu_*.jsonl")):
         shutil.copy(f, os.path.join(dst, os.path.basename(f)))
     counters, durs, sums = {}, [], {}
