@@ -75,7 +75,8 @@ VALU_PEAK_PROFILE = "profiles/r01_valu_peak.jsonl"
 # full-rate VOP2 streams 2.13): a loop of A half-rate and B full-rate
 # instructions cannot issue in fewer than A x 4.23 + B x 2.13 SIMD cycles.
 # per-variant loop mixes (tools/variant_report.py); later files add variants
-VARIANT_PROFILES = ["profiles/r02d_variant_report.jsonl", "profiles/r02k_variant_report_mode5.jsonl"]
+VARIANT_PROFILES = ["profiles/r02d_variant_report.jsonl", "profiles/r02k_variant_report_mode5.jsonl",
+                    "profiles/r03d_variant_report.jsonl"]
 VARIANT_PROFILE = ", ".join(VARIANT_PROFILES)
 IDEAL_COST_A, IDEAL_COST_B = 4.23, 2.13
 
@@ -176,7 +177,8 @@ def fast_variant(msg_len, d, k=3):
     qv = q - 64 * vb
     fv = (qv - k + 1) >> 2
     if (qv >> 2) == fv:
-        return fv, 1, trail
+        # 6 = mode 1 with the lo digits from byte 0 of word FV (a wave-uniform word)
+        return fv, 6 if (qv - k + 1) % 4 == 0 and not trail else 1, trail
     return fv, 4 if k >= 2 and ((qv - 1) >> 2) == fv else 3, trail
 
 

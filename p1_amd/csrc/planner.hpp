@@ -203,6 +203,9 @@ inline Variant fast_variant(const Layout& Y, bool split = true) {
   v.nv = (qv >> 2) - v.fv + 1;
   v.mode = 1;
   if (v.nv == 2) v.mode = !split ? 2 : (Y.k >= 2 && ((qv - 1) >> 2) == v.fv) ? 4 : 3;
+  // lo digits from byte 0: no hi digit in word FV (TRAIL stays on mode 1:
+  // its 64 trailing-block constants already fill the SGPRs)
+  else if (!Y.trail && ((qv - Y.k + 1) & 3) == 0) v.mode = 6;
   return v;
 }
 
@@ -241,6 +244,10 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
     return "internal: split variant with the units digit in the outer word";
   if (mode == 3 && dlt[1][0] != 0) return "internal: mode 3 with the tens digit in the outer word";
   if (mode == 4 && dlt[1][0] == 0) return "internal: mode 4 without the tens digit in the outer word";
+  // the kernel reads the per-nonce word of modes 6 (word FV) and 3/4 (word
+  // FV+1) from lane 0 only: no hi digit may sit in it (last hi byte: qv - k)
+  if ((mode == 6 && qv - k >= 4 * fv) || ((mode == 3 || mode == 4) && qv - k >= 4 * (fv + 1)))
+    return "internal: hi digit in the wave-uniform per-nonce word";
   FastArgs fa;
   memset(&fa, 0, sizeof fa);
   memcpy(fa.mid, P.mid, sizeof P.mid);

@@ -10,7 +10,9 @@ namespace p1 {
 // Variant id of a fast segment <FV, MODE, TRAIL> (MODE: scan_core.hpp
 // fast_thread); kGenericKind marks a generic segment.
 P1_HD constexpr uint32_t variant_id(int fv, int mode, bool trail) {
-  return mode == 5 ? 128u + (uint32_t)fv : (trail ? 64u : 0u) + (uint32_t)fv * 4u + (uint32_t)(mode - 1);
+  return mode == 5   ? 128u + (uint32_t)fv
+         : mode == 6 ? 160u + (trail ? 16u : 0u) + (uint32_t)fv
+                     : (trail ? 64u : 0u) + (uint32_t)fv * 4u + (uint32_t)(mode - 1);
 }
 constexpr uint32_t kGenericKind = 255;
 

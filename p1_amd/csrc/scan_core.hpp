@@ -161,9 +161,13 @@ P1_HD void round_half(const State& s, State& out) {
   out.v[4] = d + t1;  out.v[5] = e; out.v[6] = f; out.v[7] = g;
 }
 
-template <int FV, int NV, bool TRAIL>
+// UNI: the per-nonce word W[FV] (NV = 1) holds no hi digit, so it is the
+// same in every lane (an SGPR); the schedule sigmas of that word alone then
+// run on the SALU (sha256_dev.hpp ssig0_s/ssig1_s) instead of the VALU.
+template <int FV, int NV, bool TRAIL, bool UNI = false>
 P1_HD uint64_t fast_hash(const FastPre<FV, NV, TRAIL>& P, uint32_t wv0, uint32_t wv1, const uint32_t* kw2) {
   using FP = FastPre<FV, NV, TRAIL>;
+  static_assert(!UNI || NV == 1, "a uniform per-nonce word is the only one");
   uint32_t w[64];
 #pragma unroll
   for (int i = 0; i < 16; ++i) w[i] = (i == FV) ? wv0 : (NV == 2 && i == FV + 1) ? wv1 : P.wI[i];
@@ -180,9 +184,9 @@ P1_HD uint64_t fast_hash(const FastPre<FV, NV, TRAIL>& P, uint32_t wv0, uint32_t
 #endif
   auto sched_var = [&](int t) {
     uint32_t v = P.kw[t];
-    if (FP::var(t - 2)) v = add2(v, ssig1(w[t - 2]));
+    if (FP::var(t - 2)) v = add2(v, (UNI && t - 2 == FV) ? ssig1_s(w[t - 2]) : ssig1(w[t - 2]));
     if (FP::var(t - 7)) v = add2(v, w[t - 7]);
-    if (FP::var(t - 15)) v = add2(v, ssig0(w[t - 15]));
+    if (FP::var(t - 15)) v = add2(v, (UNI && t - 15 == FV) ? ssig0_s(w[t - 15]) : ssig0(w[t - 15]));
     if (FP::var(t - 16)) v = add2(v, w[t - 16]);
     w[t] = v;
   };
@@ -352,6 +356,10 @@ P1_HD uint32_t uniform_word(const FastArgs& A, int i) {  // the tail word after 
 //   4  hundreds and tens in FV, units in FV+1: split, W[FV] work per 10 nonces
 //   5  uniform block: PRE layout whose variable block (tail block 1) holds
 //      only the k lo digits and constants (tail bytes 64..q, k = q - 63 <= 7)
+//   6  as 1, with the lo digits from byte 0 of word FV: the word holds no hi
+//      digit, so it is wave-uniform (SGPR, SALU updates and sigmas)
+// In modes 3/4 the per-nonce word FV+1 starts with the lo digits too, so it
+// is always wave-uniform and their inner loop always runs as in mode 6.
 P1_HD constexpr int mode_nv(int mode) { return mode == 2 || mode == 3 || mode == 4 ? 2 : 1; }
 
 // Row c of a MODE 5 table: tail block 1 (`tabw`, '0' at the lo digit bytes)
@@ -459,16 +467,18 @@ P1_HD Key fast_thread_digits(const FastArgs& A, uint32_t tid) {
   for (int i = 0; i < 8; ++i) P.cv[i] = S.cv[i];
   make_pre<FV, NV, TRAIL>(P, S.Wt, uniform_word(A, FV + NV), S.wlen);
 
-  uint32_t wv0 = S.Wt[FV];
+  // mode 6: word FV has no hi digit (host-checked), so every lane holds the
+  // same value; readfirstlane makes that visible and the word an SGPR
+  uint32_t wv0 = (MODE == 6) ? wave_uniform(S.Wt[FV]) : S.Wt[FV];
   uint32_t wv1 = (NV == 2) ? S.Wt[FV + 1] : 0u;
   uint64_t best = ~0ull;
   uint32_t bestc = 0;
   uint32_t c = 0;
-  if constexpr (MODE <= 2) {
+  if constexpr (MODE <= 2 || MODE == 6) {
     for (uint32_t c2 = 0; c2 < A.n2; ++c2) {
       for (uint32_t c1 = 0; c1 < A.n1; ++c1) {
         for (uint32_t c0 = 0; c0 < 10u; ++c0) {
-          const uint64_t h = fast_hash<FV, NV, TRAIL>(P, wv0, wv1, A.kw2);
+          const uint64_t h = fast_hash<FV, NV, TRAIL, MODE == 6>(P, wv0, wv1, A.kw2);
           const bool lt = h < best;  // strict '<': first minimum wins (miner.go:59)
           best = lt ? h : best;
           bestc = lt ? c : bestc;
@@ -484,20 +494,28 @@ P1_HD Key fast_thread_digits(const FastArgs& A, uint32_t tid) {
     }
   } else {
     // split: W[FV] changes only in the hundreds (MODE 3) or tens (MODE 4)
-    // step (host-checked: du[0] == 0, and dt[0] == 0 for MODE 3)
+    // step (host-checked: du[0] == 0, and dt[0] == 0 for MODE 3).  W[FV+1]
+    // begins with the lo digits (no hi digit), so it is wave-uniform, as in
+    // mode 6 (not used with TRAIL: its 64 K+W constants already fill the
+    // SGPRs, and a uniform word there spills them).  It is re-read from lane
+    // 0 per 10 nonces: the compiler packs wv0/wv1 into one (divergent) vector
+    // for their shared carry updates.
+    constexpr bool kUni = !TRAIL;
     FastPre<FV + 1, 1, TRAIL> Q;
     for (uint32_t c2 = 0; c2 < A.n2; ++c2) {
       if (MODE == 3) outer_update<FV, TRAIL>(P, wv0, Q);
       for (uint32_t c1 = 0; c1 < A.n1; ++c1) {
         if (MODE == 4) outer_update<FV, TRAIL>(P, wv0, Q);
+        uint32_t u = kUni ? wave_uniform(wv1) : wv1;
         for (uint32_t c0 = 0; c0 < 10u; ++c0) {
-          const uint64_t h = fast_hash<FV + 1, 1, TRAIL>(Q, wv1, 0u, A.kw2);
+          const uint64_t h = fast_hash<FV + 1, 1, TRAIL, kUni>(Q, u, 0u, A.kw2);
           const bool lt = h < best;  // strict '<': first minimum wins (miner.go:59)
           best = lt ? h : best;
           bestc = lt ? c : bestc;
           ++c;
-          wv1 += A.du[1];
+          u += A.du[1];
         }
+        wv1 = u;
         if (MODE == 4) wv0 += A.dt[0];
         wv1 += A.dt[1];
       }

@@ -112,6 +112,31 @@ P1_HD uint32_t bsig1(uint32_t e) { return xor3(rotr(e, 6), rotr(e, 11), rotr(e, 
 P1_HD uint32_t ssig0(uint32_t x) { return xor3(rotr(x, 7), rotr(x, 18), x >> 3); }
 P1_HD uint32_t ssig1(uint32_t x) { return xor3(rotr(x, 17), rotr(x, 19), x >> 10); }
 
+// Scalar (wave-uniform) forms of the message-schedule sigmas: SALU shifts,
+// so a word that is the same in every lane never occupies the VALU.
+P1_HD uint32_t ssig_s(uint32_t x, int r1, int r2, int sh) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t a, b, c;
+  asm("s_lshr_b32 %0, %3, %4\n\t"
+      "s_lshl_b32 %1, %3, %5\n\t"
+      "s_or_b32 %0, %0, %1\n\t"
+      "s_lshr_b32 %1, %3, %6\n\t"
+      "s_lshl_b32 %2, %3, %7\n\t"
+      "s_or_b32 %1, %1, %2\n\t"
+      "s_xor_b32 %0, %0, %1\n\t"
+      "s_lshr_b32 %1, %3, %8\n\t"
+      "s_xor_b32 %0, %0, %1"
+      : "=&s"(a), "=&s"(b), "=&s"(c)
+      : "s"(x), "i"(r1), "i"(32 - r1), "i"(r2), "i"(32 - r2), "i"(sh)
+      : "scc");
+  return a;
+#else
+  return ((x >> r1) | (x << (32 - r1))) ^ ((x >> r2) | (x << (32 - r2))) ^ (x >> sh);
+#endif
+}
+P1_HD uint32_t ssig0_s(uint32_t x) { return ssig_s(x, 7, 18, 3); }
+P1_HD uint32_t ssig1_s(uint32_t x) { return ssig_s(x, 17, 19, 10); }
+
 // Working variables a..h of one compression.
 struct State {
   uint32_t v[8];

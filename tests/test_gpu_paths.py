@@ -64,6 +64,23 @@ def test_k3_every_layout_vs_oracle(reinit, oracle_mod):
     assert s["fast_nonces"] > 3 * s["generic_nonces"]
 
 
+def test_k2_every_layout_vs_oracle(reinit, oracle_mod):
+    """Occupancy floor 200 on 30,000-nonce ranges: k = 2 (100 nonces per
+    thread) on every layout -- the only way to run <13,1> and the k = 2
+    deltas of modes 1, 4 and 6 -- against the oracle."""
+    g = reinit(P1HIP_MIN_FAST_THREADS=200)
+    rnd = random.Random(33)
+    g.reset_stats()
+    for L in range(0, 130):
+        m = bytes(rnd.randrange(32, 127) for _ in range(L))
+        for d in (9, 10, 12):
+            lo = 10 ** (d - 1) + rnd.randrange(0, 10**5)
+            hi = lo + 29999
+            assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
+    s = g.get_stats()
+    assert s["fast_nonces"] > 3 * s["generic_nonces"]
+
+
 def test_k3_straddles_and_edges(reinit, oracle_mod):
     g = reinit(P1HIP_MIN_FAST_THREADS=1)
     rnd = random.Random(32)

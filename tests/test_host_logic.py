@@ -107,11 +107,39 @@ def test_emu_every_layout_k3(oracle_mod, nosplit, notable):
             # blocks, too many nonces for the host replay (GPU-tested instead)
             assert nf >= 1 or (q >= 69 and not notable)
             assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
-    # mode 1 runs in every pass, MODE 5 (tabulated tail block 1) unless
-    # notable; modes 3/4 only with split, mode 2 only with nosplit
-    want = {v for v in all_variants(True)
-            if (v[1] == 2) == nosplit and v[1] != 5 or v[1] == 1 or (v[1] == 5 and not notable)}
+    # modes 1 and 6 run in every pass, MODE 5 (tabulated tail block 1) unless
+    # notable; modes 3/4 only with split, mode 2 only with nosplit.  Two
+    # variants are out of reach at k = 3: <13,1> needs k = 2 (lo digits at
+    # bytes 53, 54; at k = 3 they start at byte 52: mode 6), and <0,6> is a
+    # PRE layout with lo digits at bytes 64..66, which is MODE 5 unless notable.
+    def reachable(v):
+        if v == (13, 1, 0) or (v == (0, 6, 0) and not notable):
+            return False
+        if v[1] in (1, 6):
+            return True
+        if v[1] == 5:
+            return not notable
+        return (v[1] == 2) == nosplit
+    want = {v for v in all_variants(True) if reachable(v)}
     assert seen == want, sorted(want ^ seen)
+
+
+def test_emu_every_layout_k2(oracle_mod):
+    """Occupancy floor 200 on 30,000-nonce ranges: the planner lowers k to 2
+    (100 nonces per thread), the only way to reach <13,1> (lo digits at bytes
+    53, 54) and the k = 2 deltas of every other layout; against the oracle."""
+    rnd = random.Random(9)
+    seen = set()
+    for L in range(0, 128):
+        m = bytes(rnd.randrange(32, 127) for _ in range(L))
+        for d in (9, 10, 12):
+            lo = 10 ** (d - 1) + rnd.randrange(0, 10**5)
+            hi = lo + 29999
+            got, nf, _ = emu(m, lo, hi, minthreads=200, variants=seen)
+            assert nf >= 1
+            assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
+    assert (13, 1, 0) in seen
+    assert {v[1] for v in seen} >= {1, 4, 6}  # mode 3 (hundreds alone in word FV) needs k = 3
 
 
 def _variant_cost_table():
