@@ -11,15 +11,19 @@ DEVHDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/fast_variants.in
 # device code: HIP C++ -> gfx950 assembly -> tools/isa_post.py peephole
 # (VOP2 -> VOP3 encodings of full-rate integer ops, every inner loop started
 # at 4 mod 8 bytes; see DESIGN.md "Build") -> assembled + linked code object,
-# embedded in libp1hip.so
-DEVFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) --cuda-device-only -Wall $(DEVEXTRA)
+# embedded in libp1hip.so.  The post-pass widens ~32k 4-byte instructions to
+# 8 bytes after the compiler has relaxed its branches, so the compiler is told
+# that branches reach only half their real range (+-2^15 dwords): a branch it
+# leaves short still fits after the growth; the long ones it expands are the
+# variant dispatch's, outside every loop.
+DEVFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) --cuda-device-only -Wall -mllvm -amdgpu-s-branch-bits=15 $(DEVEXTRA)
 ISAPOST ?= --align-loops=3 --loop-offset=4 --loop-parity
 BUILD := build
 
 all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios \
      tools/lsp_fake_miner tools/queue_ctl
 
-$(BUILD)/p1hip_kernels.s: $(CSRC)/p1hip_kernels.hip $(DEVHDRS)
+$(BUILD)/p1hip_kernels.s: $(CSRC)/p1hip_kernels.hip $(DEVHDRS) Makefile
 	mkdir -p $(BUILD)
 	$(HIPCC) $(DEVFLAGS) -S -o $@ $(CSRC)/p1hip_kernels.hip
 

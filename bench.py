@@ -76,7 +76,7 @@ VALU_PEAK_PROFILE = "profiles/r01_valu_peak.jsonl"
 # instructions cannot issue in fewer than A x 4.23 + B x 2.13 SIMD cycles.
 # per-variant loop mixes (tools/variant_report.py); later files add variants
 VARIANT_PROFILES = ["profiles/r02d_variant_report.jsonl", "profiles/r02k_variant_report_mode5.jsonl",
-                    "profiles/r03d_variant_report.jsonl"]
+                    "profiles/r03f_variant_report.jsonl"]
 VARIANT_PROFILE = ", ".join(VARIANT_PROFILES)
 IDEAL_COST_A, IDEAL_COST_B = 4.23, 2.13
 
@@ -170,6 +170,8 @@ def fast_variant(msg_len, d, k=3):
         vb, trail = 0, False
     elif q <= 63:
         vb, trail = 0, True
+    elif q == 64 and d > 3:
+        return 15, 7, False  # MODE 7: units alone in tail block 1 (table), tens/hundreds in block 0's W15
     elif q - 63 <= 7:
         return 0, 5, False  # MODE 5: tail block 1 holds only the lo digits (k = q - 63)
     else:
@@ -193,7 +195,12 @@ def workload_mix(msg_len, lo, hi):
         for line in open(path):
             if line.startswith("{"):
                 d = json.loads(line)
-                table[tuple(d["variant"])] = d["loop"]
+                loop = dict(d["loop"])
+                par = d.get("parent_loop_exclusive")
+                if d["variant"][1] == 7 and par:  # MODE 7: + block 0's update, once per 10 nonces
+                    loop["half_rate_A"] += par["half_rate_A"] / 10
+                    loop["full_rate_B"] += par["full_rate_B"] / 10
+                table[tuple(d["variant"])] = loop
     a = b = w = 0.0
     for d in range(1, 21):
         dlo, dhi = (0 if d == 1 else 10 ** (d - 1)), 10 ** d - 1

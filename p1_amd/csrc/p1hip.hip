@@ -370,7 +370,7 @@ constexpr int kNoTable = 1;
 int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
   for (size_t i = 0; i < d.kwtabs.size(); ++i) {
     Dev::KwTab t = d.kwtabs[i];
-    if (t.k == L.Y.k && memcmp(t.w, L.tabw, sizeof t.w) == 0) {
+    if (t.k == L.tabk && memcmp(t.w, L.tabw, sizeof t.w) == 0) {
       t.used_in = d.range_id;
       // least recently used first: a scan touches at most 7 tables (one per
       // MODE 5 decade), so it never evicts one it is about to launch with
@@ -380,7 +380,7 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
       return P1HIP_OK;
     }
   }
-  const size_t need = (size_t)pow10u(L.Y.k) * 64u * sizeof(uint32_t);
+  const size_t need = (size_t)pow10u(L.tabk) * 64u * sizeof(uint32_t);
   // P1HIP_KWTAB_MAX_BYTES (tests only): a lower cap, to exercise the re-plan
   const char* capv = getenv("P1HIP_KWTAB_MAX_BYTES");
   const size_t cap = capv && *capv ? (size_t)strtoull(capv, nullptr, 10) : kMaxKwTabBytes;
@@ -400,10 +400,10 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
   // launch that reads it is ordered after it): no host work, no upload
   Dev::KwTab t;
   memcpy(t.w, L.tabw, sizeof t.w);
-  t.k = L.Y.k;
+  t.k = L.tabk;
   t.dptr = nullptr;
   t.used_in = d.range_id;
-  const uint32_t rows = (uint32_t)pow10u(L.Y.k);
+  const uint32_t rows = (uint32_t)pow10u(L.tabk);
   const hipError_t me = hipMalloc(&t.dptr, (size_t)rows * 64u * sizeof(uint32_t));
   if (me == hipErrorOutOfMemory) {
     (void)hipGetLastError();  // not sticky: clear it and scan without the table
@@ -413,7 +413,7 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
   KwTableArgs a;
   memset(&a, 0, sizeof a);
   memcpy(a.tabw, L.tabw, sizeof a.tabw);
-  a.k = (uint32_t)L.Y.k;
+  a.k = (uint32_t)L.tabk;
   a.qv = (uint32_t)(L.Y.q - 64);
   a.rows = rows;
   a.out = t.dptr;
@@ -449,7 +449,7 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
     bool replan = false;
     for (size_t i = 0; i < plan.launches.size() && !replan; ++i) {
       const Launch& L = plan.launches[i];
-      if (!L.fast || L.mode != 5) continue;
+      if (!L.fast || (L.mode != 5 && L.mode != 7)) continue;
       const int rt = kwtable_for(d, L, &tabptr[i]);
       if (rt == kNoTable) replan = true;
       else if (rt != P1HIP_OK) return rt;
@@ -527,7 +527,7 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
         if (!has_variant(L.fv, L.mode, L.trail)) return fail(P1HIP_ERR_ARGS, "no fast kernel variant");
         S.kind = variant_id(L.fv, L.mode, L.trail);
         S.fa = L.fa;
-        if (L.mode == 5) S.fa.kwtab = tabptr[order[B.first + j]];
+        if (L.mode == 5 || L.mode == 7) S.fa.kwtab = tabptr[order[B.first + j]];
         d.fast_launches++;
         d.fast_nonces += L.nonces;
         d.fast_ops += L.nonces * kAlgOpsPerCompression * (uint64_t)L.btail;

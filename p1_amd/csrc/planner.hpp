@@ -92,19 +92,24 @@ struct Layout {
   int k;      // fast path: lo digits per thread loop
   bool trail; // fast path: a constant block follows block vb
   bool tab;   // MODE 5 allowed (tabulated block-1 schedule)
+  bool two;   // MODE 7: one digit in block 1 (table), tens/hundreds in block 0's W15; k = 3
 };
 
 // `tabulate` = false keeps layouts whose block 1 holds only lo digits on
 // the digit-update variants (k = 3 or q - 63, MODE 1) instead of MODE 5:
 // the A/B and cross-check path of P1HIP_NO_TABLE.
-inline Layout make_layout(uint32_t r, int d, bool tabulate = true) {
+// `two_level` = false keeps a one-digit block 1 on plain MODE 5 (k = 1)
+// instead of MODE 7 (ranges too small for 1000 nonces per thread).
+inline Layout make_layout(uint32_t r, int d, bool tabulate = true, bool two_level = true) {
   Layout Y;
   Y.d = d;
   Y.tab = tabulate;
+  Y.two = false;
   Y.q = (int)r + d - 1;
   Y.nb = ((int)r + d + 9 <= 64) ? 1 : 2;
   if (Y.nb == 1) { Y.vb = 0; Y.k = 3; Y.trail = false; }
   else if (Y.q <= 63) { Y.vb = 0; Y.k = 3; Y.trail = true; }     // lo digits in block 0
+  else if (tabulate && two_level && Y.q == 64 && d > 3) { Y.vb = 1; Y.k = 3; Y.trail = false; Y.two = true; }  // MODE 7
   else if (tabulate && Y.q - 63 <= kMaxTabDigits) { Y.vb = 1; Y.k = Y.q - 63; Y.trail = false; }  // MODE 5
   else if (Y.q - 64 >= 2) { Y.vb = 1; Y.k = 3; Y.trail = false; }                // lo digits in block 1
   else { Y.vb = 1; Y.k = Y.q - 63; Y.trail = false; }                            // q in {64,65}: k = 1, 2
@@ -143,6 +148,7 @@ struct Launch {
   // filled in by whoever runs the plan (a device copy in p1hip.hip, a host
   // copy in tools/p1emu)
   uint32_t tabw[16];  // tail block 1 words, '0' at the lo digit bytes
+  int tabk;           // MODE 5 / 7: digits the table covers (10^tabk rows; MODE 7: 1)
 };
 
 struct Plan {
@@ -193,6 +199,12 @@ struct Variant {
 inline Variant fast_variant(const Layout& Y, bool split = true) {
   const int qv = Y.q - 64 * Y.vb;
   Variant v;
+  if (Y.two) {  // MODE 7: the per-nonce word of block 0 is W15
+    v.fv = 15;
+    v.nv = 1;
+    v.mode = 7;
+    return v;
+  }
   if (Y.tab && Y.vb == 1 && Y.q - 63 == Y.k) {  // tail block 1 holds only lo digits (W[0], W[1]) and constants
     v.fv = 0;
     v.nv = 1;
@@ -232,10 +244,22 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
   // the digit-update modes handle k <= 3; only MODE 5 (tabulated) takes k = 4..7
   if (k > 3 && var.mode != 5) return "internal: more than 3 lo digits outside MODE 5";
   uint32_t dlt[3][2] = {{0, 0}, {0, 0}, {0, 0}};  // per lo digit (units, tens, hundreds)
-  for (int t = 0; t < k && t < 3; ++t) {
-    const int p = qv - t;
-    const int slot = (p >> 2) - fv;
-    dlt[t][slot] = 1u << (24 - 8 * (p & 3));
+  if (var.mode == 7) {
+    // units: tail byte 64 (block 1, from the table); tens, hundreds: bytes 63,
+    // 62 = the low bytes of block 0's W15; block 1 = units, 0x80, zeros, length
+    if (Y.q != 64 || k != 3) return "internal: MODE 7 layout";
+    if (tmpl[16] != 0x30800000u) return "internal: MODE 7 block 1 word 0";
+    for (int i = 17; i < 30; ++i)
+      if (tmpl[i] != 0u) return "internal: MODE 7 block 1 not empty";
+    if ((tmpl[15] & 0xffffu) != 0x3030u) return "internal: MODE 7 tens/hundreds not in W15";
+    dlt[1][0] = 1u;
+    dlt[2][0] = 1u << 8;
+  } else {
+    for (int t = 0; t < k && t < 3; ++t) {
+      const int p = qv - t;
+      const int slot = (p >> 2) - fv;
+      dlt[t][slot] = 1u << (24 - 8 * (p & 3));
+    }
   }
   // units are always in the last word; mode 3 = only the hundreds digit in
   // word FV, mode 4 = tens (and hundreds) in word FV
@@ -260,7 +284,7 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
   }
   fa.dh = (uint32_t)(Y.d - k);
   fa.p_last = (uint32_t)(Y.q - k);
-  fa.pre = (uint32_t)Y.vb;
+  fa.pre = mode == 7 ? 0u : (uint32_t)Y.vb;  // MODE 7 steps block 0 (W15); its block 1 is the table
   fa.kpow = (uint32_t)pow10u(k);
   fa.nsub = (mode == 5 && k > 3) ? (uint32_t)pow10u(k - 3) : 1u;
   fa.n1 = k >= 2 ? 10u : 1u;
@@ -293,7 +317,8 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
     Ln.nonces = cnt * fa.kpow;
     Ln.btail = Y.nb;
     Ln.Y = Y;
-    if (mode == 5) memcpy(Ln.tabw, tmpl + 16, sizeof Ln.tabw);
+    if (mode == 5 || mode == 7) memcpy(Ln.tabw, tmpl + 16, sizeof Ln.tabw);
+    Ln.tabk = mode == 5 ? k : mode == 7 ? 1 : 0;
     Ln.fa.part_off = plan.total_blocks;
     plan.total_blocks += Ln.blocks;
     plan.total_nonces += Ln.nonces;
@@ -309,7 +334,7 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
 // row[0] = W[0] (round 0's per-thread half already holds K[0]), row[t] =
 // K[t] + W[t] for t >= 1, W = tail block 1 with c's k digits in place.
 inline std::vector<uint32_t> build_kwtable(const Launch& L) {
-  const int k = L.Y.k;
+  const int k = L.tabk;
   const int qv = L.Y.q - 64;
   const uint32_t rows = (uint32_t)pow10u(k);
   std::vector<uint32_t> tab((size_t)rows * 64u);
@@ -368,6 +393,8 @@ inline std::string make_plan(const uint8_t* msg, size_t L, uint64_t lower, uint6
     // runs at most 10^3 nonces (MODE 5 splits k > 3 into runs of 1000), so a
     // MODE 5 layout that is too small goes straight to the k = 3 digit layout
     if (Y.k > 3 && (e - s) / 1000u + 1 < min_fast_threads) Y = make_layout(P.r, d, false);
+    // MODE 7 runs 1000 nonces per thread; too small a decade takes plain MODE 5 at k = 1
+    if (Y.two && (e - s) / 1000u + 1 < min_fast_threads) Y = make_layout(P.r, d, tabulate, false);
     if (Y.k <= 3)
       while (Y.k > 1 && (e - s) / pow10u(Y.k) + 1 < min_fast_threads) --Y.k;
     if (!fast_ok || d <= Y.k) {

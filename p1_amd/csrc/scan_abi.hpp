@@ -11,6 +11,7 @@ namespace p1 {
 // fast_thread); kGenericKind marks a generic segment.
 P1_HD constexpr uint32_t variant_id(int fv, int mode, bool trail) {
   return mode == 5   ? 128u + (uint32_t)fv
+         : mode == 7 ? 192u + (uint32_t)fv
          : mode == 6 ? 160u + (trail ? 16u : 0u) + (uint32_t)fv
                      : (trail ? 64u : 0u) + (uint32_t)fv * 4u + (uint32_t)(mode - 1);
 }

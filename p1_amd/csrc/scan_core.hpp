@@ -164,8 +164,10 @@ P1_HD void round_half(const State& s, State& out) {
 // UNI: the per-nonce word W[FV] (NV = 1) holds no hi digit, so it is the
 // same in every lane (an SGPR); the schedule sigmas of that word alone then
 // run on the SALU (sha256_dev.hpp ssig0_s/ssig1_s) instead of the VALU.
+// The variable block's rounds FV..63 for one nonce: its working state after
+// round 63 (not yet added to the chaining value P.cv).
 template <int FV, int NV, bool TRAIL, bool UNI = false>
-P1_HD uint64_t fast_hash(const FastPre<FV, NV, TRAIL>& P, uint32_t wv0, uint32_t wv1, const uint32_t* kw2) {
+P1_HD State fast_rounds(const FastPre<FV, NV, TRAIL>& P, uint32_t wv0, uint32_t wv1) {
   using FP = FastPre<FV, NV, TRAIL>;
   static_assert(!UNI || NV == 1, "a uniform per-nonce word is the only one");
   uint32_t w[64];
@@ -203,6 +205,12 @@ P1_HD uint64_t fast_hash(const FastPre<FV, NV, TRAIL>& P, uint32_t wv0, uint32_t
     if (kJit && t >= 16 && FP::var(t)) sched_var(t);
     sha_round(s, FP::var(t) ? k256(t) + w[t] : P.kw[t]);
   }
+  return s;
+}
+
+template <int FV, int NV, bool TRAIL, bool UNI = false>
+P1_HD uint64_t fast_hash(const FastPre<FV, NV, TRAIL>& P, uint32_t wv0, uint32_t wv1, const uint32_t* kw2) {
+  const State s = fast_rounds<FV, NV, TRAIL, UNI>(P, wv0, wv1);
   if constexpr (!TRAIL) {
     return ((uint64_t)(P.cv[0] + s.v[0]) << 32) | (uint64_t)(P.cv[1] + s.v[1]);
   } else {
@@ -358,6 +366,10 @@ P1_HD uint32_t uniform_word(const FastArgs& A, int i) {  // the tail word after 
 //      only the k lo digits and constants (tail bytes 64..q, k = q - 63 <= 7)
 //   6  as 1, with the lo digits from byte 0 of word FV: the word holds no hi
 //      digit, so it is wave-uniform (SGPR, SALU updates and sigmas)
+//   7  two-level MODE 5: the last digit alone is in tail block 1 (byte 64),
+//      the tens and hundreds at bytes 62, 63 of block 0 (W15): per 10 nonces
+//      block 0's rounds 15..63 (the `15,1` update), per nonce block 1 from a
+//      10-row table (FV = 15: the variable word of block 0)
 // In modes 3/4 the per-nonce word FV+1 starts with the lo digits too, so it
 // is always wave-uniform and their inner loop always runs as in mode 6.
 P1_HD constexpr int mode_nv(int mode) { return mode == 2 || mode == 3 || mode == 4 ? 2 : 1; }
@@ -417,6 +429,66 @@ P1_HD uint32_t wave_uniform(uint32_t x) {
 #endif
 }
 
+// One nonce of a MODE 5 / MODE 7 block: s1 = the block's state after the
+// per-thread half of round 0, cv = its chaining value, row = the lo value's
+// table row (scalar loads).  Returns bitcoin.Hash's 64-bit value.
+P1_HD uint64_t table_block(const State& s1, const uint32_t* cv, const uint32_t* row) {
+  State s = s1;
+  const uint32_t w0 = ld_uniform(row, 0);
+  s.v[0] = add2(s.v[0], w0);
+  s.v[4] = add2(s.v[4], w0);
+#pragma unroll
+  for (int t = 1; t < 64; ++t) sha_round(s, ld_uniform(row, (uint32_t)t));
+  return ((uint64_t)(cv[0] + s.v[0]) << 32) | (uint64_t)(cv[1] + s.v[1]);
+}
+
+// MODE 7 (two-level MODE 5, one digit in tail block 1).  A thread owns
+// hi = nonce / 1000: its digits fill block 0 up to byte 61, the hundreds and
+// tens digits are bytes 62, 63 (W15 of block 0, '0' in the template and
+// ASCII-stepped like mode 1's per-nonce word), the units digit is byte 64 =
+// tail block 1, whose schedule is the 10-row MODE 5 table.  Per thread:
+// block 0's rounds 0..14 and its W15-invariant schedule (make_pre<15,1>).
+// Per tens value: rounds 15..63 of block 0 -> block 1's chaining value and
+// the per-thread half of its round 0.  Per nonce: block 1's rounds 1..63.
+// Plain MODE 5 at k = 1 recompresses the whole of block 0 every 10 nonces.
+P1_HD Key fast_thread_two(const FastArgs& A, uint32_t tid) {
+  FastSetup S;
+  fast_setup(A, tid, S);  // pre = 0: S.Wt = block 0 with the hi digits, S.cv = midstate
+  FastPre<15, 1, false> P;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) P.cv[i] = S.cv[i];
+  make_pre<15, 1, false>(P, S.Wt, 0u, 0u);
+  const uint32_t* tab = (const uint32_t*)(uintptr_t)A.kwtab;
+  uint32_t w15 = S.Wt[15];
+  uint64_t best = ~0ull;
+  uint32_t bestc = 0;
+  uint32_t c = 0;
+  for (uint32_t c2 = 0; c2 < 10u; ++c2) {
+    for (uint32_t c1 = 0; c1 < 10u; ++c1) {
+      const State s0 = fast_rounds<15, 1, false>(P, w15, 0u);
+      uint32_t cv1[8];
+      State b0, b1;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b0.v[i] = cv1[i] = P.cv[i] + s0.v[i];
+      round_half<0>(b0, b1);
+#pragma nounroll
+      for (uint32_t u = 0; u < 10u; ++u) {
+        const uint64_t h = table_block(b1, cv1, tab + (size_t)u * 64u);
+        const bool lt = h < best;  // strict '<': first minimum wins (miner.go:59)
+        best = lt ? h : best;
+        bestc = lt ? c : bestc;
+        ++c;
+      }
+      w15 += A.dt[0];
+    }
+    w15 += A.dhd[0];
+  }
+  Key k;
+  k.h = S.valid ? best : ~0ull;
+  k.n = S.valid ? S.hi * (uint64_t)A.kpow + bestc : ~0ull;
+  return k;
+}
+
 // With k = 4..7 the 10^k lo values of a hi are split into nsub = 10^(k-3)
 // runs of 1000 rows (the same thread length as k = 3, so a 2^32-nonce scan
 // still has thousands of workgroups).  The run index must be uniform per wave
@@ -439,14 +511,7 @@ P1_HD Key fast_thread_uniform(const FastArgs& A, uint32_t tid) {
   uint64_t best = ~0ull;
   uint32_t bestc = 0;
   for (uint32_t c = c0; c < c0 + per; ++c) {
-    const uint32_t* row = tab + (size_t)c * 64u;
-    State s = s1;
-    const uint32_t w0 = ld_uniform(row, 0);
-    s.v[0] = add2(s.v[0], w0);
-    s.v[4] = add2(s.v[4], w0);
-#pragma unroll
-    for (int t = 1; t < 64; ++t) sha_round(s, ld_uniform(row, (uint32_t)t));
-    const uint64_t h = ((uint64_t)(S.cv[0] + s.v[0]) << 32) | (uint64_t)(S.cv[1] + s.v[1]);
+    const uint64_t h = table_block(s1, S.cv, tab + (size_t)c * 64u);
     const bool lt = h < best;  // strict '<': first minimum wins (miner.go:59)
     best = lt ? h : best;
     bestc = lt ? c : bestc;
@@ -534,6 +599,9 @@ P1_HD Key fast_thread(const FastArgs& A, uint32_t tid) {
   if constexpr (MODE == 5) {
     static_assert(FV == 0 && !TRAIL, "MODE 5 is the whole tail block 1");
     return fast_thread_uniform(A, tid);
+  } else if constexpr (MODE == 7) {
+    static_assert(FV == 15 && !TRAIL, "MODE 7 steps W15 of block 0");
+    return fast_thread_two(A, tid);
   } else {
     return fast_thread_digits<FV, MODE, TRAIL>(A, tid);
   }

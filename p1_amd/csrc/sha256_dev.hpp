@@ -5,11 +5,13 @@
 //   Ch / Maj  -> one v_bitop3_b32 each (truth tables 0xCA / 0xE8)
 //   xor3      -> one v_bitop3_b32 (0x96) for the three rotations of S0/S1/s0/s1
 //   T1, a'    -> v_add3_u32 (selected by the compiler from the '+' chains)
-// gfx950 has no bitop3 builtin and LLVM does not reliably form it inside the
-// round's sums, so the three are one-line inline asm (convergent for the
-// compiler: it never hoists them, so fast_thread hoists invariants by hand).  Every helper folds to a constant when its inputs are
-// compile-time constants (`__builtin_constant_p`, resolved after
-// unrolling/inlining), so zero words of the message schedule cost nothing.
+// LLVM does not reliably form bitop3 from C inside the round's sums, so the
+// three are the gfx950 builtin __builtin_amdgcn_bitop3_b32 (r01-r03e: one-line
+// inline asm; the compiler then had to pad hazard s_nops after the opaque asm
+// -- 57 per nonce in the MODE 7 loop -- and never hoisted it, which is why
+// fast_thread hoists invariants by hand).  Every helper folds to a constant
+// when its inputs are compile-time constants (`__builtin_constant_p`,
+// resolved after unrolling/inlining), so zero words of the schedule cost nothing.
 //
 // The helpers are __host__ __device__ only so that tools/p1emu can run the
 // exact per-thread scan logic on the host for layout tests; the host branch
@@ -65,11 +67,7 @@ P1_HD uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
 
 P1_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (!P1_CONST3(a, b, c)) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-  }
+  if (!P1_CONST3(a, b, c)) return (uint32_t)__builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 #endif
   return a ^ b ^ c;
 }
@@ -79,11 +77,7 @@ P1_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // and + add and the loop grows by ~100 instructions per nonce -- measured.)
 P1_HD uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (!P1_CONST3(e, f, g)) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(e), "v"(f), "v"(g));
-    return r;
-  }
+  if (!P1_CONST3(e, f, g)) return (uint32_t)__builtin_amdgcn_bitop3_b32(e, f, g, 0xca);
 #endif
   return (e & f) ^ (~e & g);
 }
@@ -91,11 +85,7 @@ P1_HD uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
 // Maj(a,b,c) = (a & b) ^ (a & c) ^ (b & c)
 P1_HD uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (!P1_CONST3(a, b, c)) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-  }
+  if (!P1_CONST3(a, b, c)) return (uint32_t)__builtin_amdgcn_bitop3_b32(a, b, c, 0xe8);
 #endif
   return (a & b) ^ (a & c) ^ (b & c);
 }

@@ -168,12 +168,49 @@ def test_mode5_whole_blocks_vs_oracle(reinit, oracle_mod):
     assert s["fast_nonces"] > 0.9 * n_all  # the whole blocks ran in fast (MODE 5) segments
 
 
+def test_mode7_two_level_vs_oracle(reinit, oracle_mod, monkeypatch):
+    """MODE 7: the last digit alone in tail block 1 (q = 64), the tens and
+    hundreds stepped in block 0's W15, 1000 nonces per thread.  Exactly
+    against the oracle over whole 1000-blocks plus ragged edges for every
+    (L + 1) % 64 that puts a 4..20-digit nonce there, and on 10^7-nonce
+    ranges against plain MODE 5 at k = 1 (what a decade too small for 1000
+    nonces per thread runs: the default occupancy floor) and the digit
+    variants (P1HIP_NO_TABLE)."""
+    rnd = random.Random(36)
+    small, big = [], []
+    for r in (45, 48, 50, 55, 57, 60, 63):
+        d = 65 - r
+        m = bytes(rnd.randrange(32, 127) for _ in range(r - 1 + 64 * rnd.randrange(0, 2)))
+        base = 10 ** (d - 1) + rnd.randrange(1, 90) * 1000
+        small.append((m, base - 321, base + 3000 + 432))
+        if d >= 9:
+            lo = 10 ** (d - 1) + rnd.randrange(0, 10**6)
+            big.append((m, lo, lo + 10**7))
+    g = reinit(P1HIP_MIN_FAST_THREADS=1)
+    g.reset_stats()
+    for m, lo, hi in small:
+        assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=16), (len(m), lo, hi)
+    s = g.get_stats()
+    assert s["fast_nonces"] > 0.7 * s["scan_nonces"] and s["table_replans"] == 0
+    two = [g.scan(m, lo, hi) for m, lo, hi in big]
+    monkeypatch.delenv("P1HIP_MIN_FAST_THREADS")
+    g = reinit()  # default floor: 10^7 nonces are < 2^18 threads of 1000, so plain MODE 5 at k = 1
+    plain = [g.scan(m, lo, hi) for m, lo, hi in big]
+    g = reinit(P1HIP_NO_TABLE=1, P1HIP_MIN_FAST_THREADS=1)
+    digits = [g.scan(m, lo, hi) for m, lo, hi in big]
+    assert two == plain == digits
+    for (m, lo, hi), (h, n) in zip(big, two):
+        assert lo <= n <= hi and oracle_mod.hash(m, n) == h
+
+
 def test_mode5_replan_before_any_launch(reinit, oracle_mod, monkeypatch):
     """a MODE 5 table that cannot be had is found in a
-    pre-pass, before any k_scan of the share is enqueued.  The MODE 5 piece
-    (k = 1, weight 20) sorts behind a k = 3 TRAIL piece, so under a small
-    per-launch cap it lands in launch >= 2 -- where the old code re-planned
-    after launch 1 was already queued.  Now: the answer is the oracle's, one
+    pre-pass, before any k_scan of the share is enqueued.  The table piece
+    (one digit in block 1: MODE 7 since r03f, weight 2000, equal to the
+    TRAIL piece's, so it keeps its later place in plan order; plain MODE 5 at
+    k = 1 before, weight 20) sorts behind a k = 3 TRAIL piece, so under a
+    small per-launch cap it lands in launch >= 2 -- where the old code
+    re-planned after launch 1 was already queued.  Now: the answer is the oracle's, one
     re-plan is counted, every nonce is scanned once, and the launches are
     exactly those of the same scan planned without MODE 5 at all."""
     m = bytes(range(65, 65 + 53))  # L = 53: r = 54, d = 10 TRAIL (k = 3), d = 11 MODE 5 with k = 1

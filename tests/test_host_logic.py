@@ -107,8 +107,8 @@ def test_emu_every_layout_k3(oracle_mod, nosplit, notable):
             # blocks, too many nonces for the host replay (GPU-tested instead)
             assert nf >= 1 or (q >= 69 and not notable)
             assert got == oracle_mod.scan(m, lo, hi, threads=8), (L, d, lo, hi)
-    # modes 1 and 6 run in every pass, MODE 5 (tabulated tail block 1) unless
-    # notable; modes 3/4 only with split, mode 2 only with nosplit.  Two
+    # modes 1 and 6 run in every pass, MODEs 5 and 7 (tabulated tail block 1)
+    # unless notable; modes 3/4 only with split, mode 2 only with nosplit.  Two
     # variants are out of reach at k = 3: <13,1> needs k = 2 (lo digits at
     # bytes 53, 54; at k = 3 they start at byte 52: mode 6), and <0,6> is a
     # PRE layout with lo digits at bytes 64..66, which is MODE 5 unless notable.
@@ -117,7 +117,7 @@ def test_emu_every_layout_k3(oracle_mod, nosplit, notable):
             return False
         if v[1] in (1, 6):
             return True
-        if v[1] == 5:
+        if v[1] in (5, 7):  # tabulated tail block 1
             return not notable
         return (v[1] == 2) == nosplit
     want = {v for v in all_variants(True) if reachable(v)}

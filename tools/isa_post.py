@@ -23,9 +23,9 @@ scan-kernel A/Bs in profiles/r01n_e64_ab.jsonl, profiles/r01r_loop_offset_sweep.
    costs ~4.2 cycles (the full-rate ones lose their advantage).  Measured on
    the c2 scan kernel: loop start at 4 mod 8 -> 36.3 GH/s, at 0 mod 8 ->
    32.1 GH/s, every 4-byte step of a 64-byte sweep.
-   --align-loops=3 --loop-offset=4 puts each inner-loop label at 4 (mod 8)
+   --align-loops=3 --loop-offset=4 puts each loop label at 4 (mod 8)
    (`.p2align 3` + one `s_nop 0` executed once on loop entry).
-   --loop-parity additionally walks each inner-loop body with exact
+   --loop-parity additionally walks each loop body with exact
    instruction sizes (from llvm-mc) and restores the parity after every
    4-byte instruction that breaks it: by widening the preceding 4-byte VALU
    (VOP1/VOP2/VOPC e32 -> e64, same operands) where possible, else by
@@ -113,20 +113,21 @@ def sizes_of(instrs, cpu="gfx950"):
     return [len(e.split("; encoding: [")[1].rstrip("]").split(",")) for e in enc]
 
 
-def loop_headers(lines):
-    """Indices of inner-loop header labels (LLVM's loop comments)."""
+def loop_headers(lines, tag="Loop Header"):
+    """Indices of loop header labels (LLVM's loop comments): every loop with
+    the default tag, innermost loops only with tag="Inner Loop Header"."""
     hdr = []
     for i, ln in enumerate(lines):
         if not RE_LABEL.match(ln):
             continue
-        if "Inner Loop Header" in ln:
+        if tag in ln:
             hdr.append(i)
             continue
         for ln2 in lines[i + 1:]:
             t = ln2.strip()
             if t and not t.startswith(";"):
                 break
-            if "Inner Loop Header" in t:
+            if tag in t:
                 hdr.append(i)
                 break
     return hdr
@@ -180,8 +181,11 @@ def pass_align(lines, align, offset, stats):
 
 
 def pass_parity(lines, stats):
-    """Inner-loop bodies (label .. branch back to it) start at 4 mod 8 (pass_align
-    with offset 4); keep every 8-byte instruction in them at 4 mod 8."""
+    """Loop bodies (label .. branch back to it) start at 4 mod 8 (pass_align
+    with offset 4); keep every 8-byte instruction in them at 4 mod 8.  Loops
+    nest: a line belongs to its innermost loop, whose header re-synchronises
+    the position; an outer loop's own instructions (e.g. MODE 7's block-0
+    update around its table loop) continue from where its inner loop ends."""
     regions = []
     for h in loop_headers(lines):
         label = RE_LABEL.match(lines[h]).group(1)
@@ -193,7 +197,7 @@ def pass_parity(lines, stats):
     body_idx = [k for a, b in regions for k in range(a + 1, b + 1) if is_instr(lines[k].strip())]
     size = dict(zip(body_idx, sizes_of([lines[k].strip() for k in body_idx])))
     in_region = {}
-    for a, b in regions:
+    for a, b in sorted(regions, key=lambda r: r[0] - r[1]):  # outermost first: inner loops overwrite
         for k in range(a + 1, b + 1):
             in_region[k] = a
     out = []

@@ -11,6 +11,7 @@ the shipped pipeline (hipcc -S -> tools/isa_post.py -> code object) and read
     v_add3_u32 and the other 3-input VOP3 integer ops) and full-rate "B" --
     SALU instructions, bytes, and how many 8-byte instructions sit at
     4 (mod 8);
+  * the enclosing loop's own instructions (inner loop excluded), per trip;
   * a predicted rate from the measured issue costs (A 4.37,
     B 2.66 SIMD cycles per wave instruction at 4 waves/SIMD) at 2.35 GHz.
 
@@ -73,11 +74,17 @@ def loops_of(co, kern="k_scan"):
             if tgt < a:
                 loops.append((tgt, a))
     inner = [l for l in loops if not any(o != l and l[0] <= o[0] and o[1] <= l[1] for o in loops)]
-    return ins, inner
+    return ins, inner, loops
 
 
-def mix(ins, lo, hi):
-    body = [(a, sz, t) for a, sz, t in ins if lo <= a <= hi]
+def parent_of(loop, loops):
+    """The smallest loop strictly containing `loop` (None at top level)."""
+    outer = [o for o in loops if o != loop and o[0] <= loop[0] and loop[1] <= o[1]]
+    return min(outer, key=lambda o: o[1] - o[0]) if outer else None
+
+
+def mix(ins, lo, hi, exclude=None):
+    body = [(a, sz, t) for a, sz, t in ins if lo <= a <= hi and not (exclude and exclude[0] <= a <= exclude[1])]
     A = B = S = other = n8 = at4 = 0
     for a, sz, t in body:
         op = t.split()[0]
@@ -119,9 +126,15 @@ def build_one(v, waves, isapost):
         subprocess.run([f"{LLVM}/ld.lld", "-m", "elf64_amdgpu", "--no-undefined", "-shared", "-o", co, o], check=True)
         r = {"variant": [fv, nv, tr]}
         r.update(meta(open(s).read()))
-        ins, inner = loops_of(co)
+        ins, inner, loops = loops_of(co)
         big = max(inner, key=lambda l: l[1] - l[0])
         r["loop"] = mix(ins, *big)
+        # the enclosing loop's own instructions (per trip of it, the inner
+        # loop excluded): MODE 7's per-10-nonce block-0 update, the split
+        # modes' outer_update
+        par = parent_of(big, loops)
+        if par:
+            r["parent_loop_exclusive"] = mix(ins, par[0], par[1], exclude=big)
         r["waves_per_simd_vgpr"] = min(8, 512 // max(1, r["vgpr"]))
         r["blocks_per_cu_sgpr"] = min(8, 800 // ((-(-r["sgpr"] // 16)) * 16 + 16))
         return r
