@@ -40,7 +40,7 @@ static Key run_fast(const FastArgs& A, uint64_t threads) {
 static Key dispatch_fast(const Launch& L0) {
   Launch L = L0;
   std::vector<uint32_t> tab;  // MODE 5: the K+W table, here in host memory
-  if (L.mode == 5) {
+  if (L.mode == 5 || L.mode == 7) {
     tab = build_kwtable(L);
     L.fa.kwtab = (uint64_t)(uintptr_t)tab.data();
   }
