@@ -22,7 +22,15 @@
 //     flight are ignored when they arrive);
 //   * a request's answer is the lexicographic (hash, nonce) min over its
 //     chunks with miner.go:56's identity (MaxUint64, 0) -- identical to one
-//     miner scanning the whole range (contiguous chunks, strict '<').
+//     miner scanning the whole range (contiguous chunks, strict '<');
+//   * optional tail hedging (SetHedge(2), `p1server --hedge`): once no
+//     request has an unsent chunk, an idle miner gets a copy of the chunk
+//     that has been in flight longest (at most `copies` miners per chunk).
+//     The first Result for a chunk counts and later copies are ignored; a
+//     scan is deterministic, so every copy has the same answer.  Under loss
+//     a Request or Result datagram is only resent one LSP epoch later
+//     (2 s by default), which leaves a job waiting on one chunk while the
+//     other miners idle; a copy on an idle miner ends that wait.
 #pragma once
 #include <stdint.h>
 
@@ -78,15 +86,33 @@ class Scheduler {
     }
   }
 
+  // At most `copies` miners run one chunk (1 = no hedging, the default).
+  void SetHedge(int copies) { copies_ = copies < 1 ? 1 : copies; }
+
   void AddMiner(int miner) { miners_[miner]; }  // idle (server.go:153-166)
   bool IsMiner(int miner) const { return miners_.count(miner) != 0; }
   size_t Miners() const { return miners_.size(); }
 
-  // A miner is lost: its chunk goes back to the front of its request.
+  // A miner is lost: its chunk goes back to the front of its request --
+  // unless another miner still runs a copy of it, or it is already answered.
   void LoseMiner(int miner) {
     auto it = miners_.find(miner);
     if (it == miners_.end()) return;
-    if (it->second.busy) requeue(it->second.cur_req, it->second.lo, it->second.hi);
+    const Miner& m = it->second;
+    if (m.busy) {
+      auto r = reqs_.find(m.cur_req);
+      if (r != reqs_.end()) {
+        auto f = r->second.inflight.find(m.lo);
+        if (f != r->second.inflight.end()) {
+          if (f->second.copies > 1) {
+            f->second.copies--;
+          } else {
+            r->second.inflight.erase(f);
+            r->second.back.push_front({m.lo, m.hi});
+          }
+        }
+      }
+    }
     miners_.erase(it);
   }
 
@@ -100,8 +126,10 @@ class Scheduler {
     auto r = reqs_.find(m.cur_req);
     if (r == reqs_.end()) return true;  // its client is gone
     Req& q = r->second;
-    q.outstanding--;
-    if (!q.has_work() && q.outstanding == 0) done_.push_back(q.id);
+    auto f = q.inflight.find(m.lo);
+    if (f == q.inflight.end()) return true;  // a copy already answered this chunk
+    q.inflight.erase(f);
+    if (!q.has_work() && q.inflight.empty()) done_.push_back(q.id);
     // a chunk whose hashes are all MaxUint64 reports (Max, 0); only real
     // minima (< Max) take part, lexicographically -- identity of miner.go:56
     if (hash < UINT64_MAX && (!q.found || hash < q.best || (hash == q.best && nonce < q.best_n))) {
@@ -112,7 +140,8 @@ class Scheduler {
     return true;
   }
 
-  // Hand one chunk to every idle miner, round-robin over open requests.
+  // Hand one chunk to every idle miner, round-robin over open requests;
+  // with hedging, idle miners left over get copies of the oldest chunks.
   std::vector<Assignment> Dispatch() {
     std::vector<Assignment> out;
     for (auto& kv : miners_) {
@@ -125,16 +154,12 @@ class Scheduler {
         if (it == reqs_.end() || !it->second.has_work()) continue;
         Req& r = it->second;
         const Span c = r.take(chunk_);
-        r.outstanding++;
-        m.busy = true;
-        m.cur_req = id;
-        m.lo = c.lo;
-        m.hi = c.hi;
-        out.push_back({kv.first, id, r.data, c.lo, c.hi});
+        r.inflight[c.lo] = {c.hi, 1, seq_++};
+        assign(kv.first, m, r, c.lo, c.hi, out);
         any = true;
         break;
       }
-      if (!any) break;
+      if (!any && !hedge_one(kv.first, m, out)) break;
     }
     return out;
   }
@@ -158,6 +183,15 @@ class Scheduler {
     return out;
   }
 
+  // Miners running a copy of the chunk of `req` that starts at `lo` (0 if
+  // none: unsent or answered).  Tests use it.
+  int Copies(uint64_t req, uint64_t lo) const {
+    auto it = reqs_.find(req);
+    if (it == reqs_.end()) return 0;
+    auto f = it->second.inflight.find(lo);
+    return f == it->second.inflight.end() ? 0 : f->second.copies;
+  }
+
   // Chunks a request still holds in memory (handed-back chunks; the unsent
   // rest of its range is one cursor).  Tests bound this.
   size_t HeldSpans(uint64_t req) const {
@@ -173,6 +207,11 @@ class Scheduler {
   struct Span {
     uint64_t lo, hi;
   };
+  struct Flight {     // a chunk sent to at least one miner, not answered yet
+    uint64_t hi;
+    int copies;       // miners running it
+    uint64_t seq;     // dispatch order of its first copy (oldest is hedged first)
+  };
   struct Req {
     uint64_t id;
     int64_t client;
@@ -180,7 +219,7 @@ class Scheduler {
     std::deque<Span> back;       // chunks handed back by lost miners (sent first)
     uint64_t next = 0, hi = 0;   // cursor: [next, hi] not handed out yet
     bool exhausted = false;      // the cursor has passed hi
-    uint64_t outstanding = 0;
+    std::map<uint64_t, Flight> inflight;  // by chunk lo
     uint64_t best = UINT64_MAX, best_n = 0;
     bool found = false;
     bool has_work() const { return !back.empty() || !exhausted; }
@@ -203,11 +242,32 @@ class Scheduler {
     uint64_t cur_req = 0, lo = 0, hi = 0;
   };
 
-  void requeue(uint64_t req, uint64_t lo, uint64_t hi) {
-    auto it = reqs_.find(req);
-    if (it == reqs_.end()) return;
-    it->second.outstanding--;
-    it->second.back.push_front({lo, hi});
+  static void assign(int id, Miner& m, const Req& r, uint64_t lo, uint64_t hi, std::vector<Assignment>& out) {
+    m.busy = true;
+    m.cur_req = r.id;
+    m.lo = lo;
+    m.hi = hi;
+    out.push_back({id, r.id, r.data, lo, hi});
+  }
+  // Give idle miner `id` a copy of the oldest in-flight chunk that has fewer
+  // than copies_ miners; false if there is none (or hedging is off).
+  bool hedge_one(int id, Miner& m, std::vector<Assignment>& out) {
+    if (copies_ <= 1) return false;
+    Req* best_r = nullptr;
+    std::map<uint64_t, Flight>::iterator best_f;
+    for (auto& kv : reqs_) {
+      for (auto f = kv.second.inflight.begin(); f != kv.second.inflight.end(); ++f) {
+        if (f->second.copies >= copies_) continue;
+        if (!best_r || f->second.seq < best_f->second.seq) {
+          best_r = &kv.second;
+          best_f = f;
+        }
+      }
+    }
+    if (!best_r) return false;
+    best_f->second.copies++;
+    assign(id, m, *best_r, best_f->first, best_f->second.hi, out);
+    return true;
   }
   void drop_order(uint64_t id) {
     for (size_t i = 0; i < order_.size(); ++i)
@@ -224,6 +284,8 @@ class Scheduler {
   std::vector<uint64_t> done_;  // completed request ids, in completion order
   size_t rr_ = 0;
   uint64_t next_id_ = 1;
+  uint64_t seq_ = 0;
+  int copies_ = 1;
 };
 
 }  // namespace sched
