@@ -9,7 +9,7 @@ result equals the min of the two halves scanned separately).  Runs with the
 production settings (one-launch small path, MODE 5 tables, default occupancy
 floor).  Prints one JSON summary line.
 
-usage: python tools/stress.py [seconds] [seed]
+usage: [STRESS_MAXLEN=n] python tools/stress.py [seconds] [seed]
 """
 import json
 import os
@@ -26,8 +26,11 @@ import p1_amd  # noqa: E402
 U64_MAX = (1 << 64) - 1
 
 
+MAX_LEN = int(os.environ.get("STRESS_MAXLEN", "200"))  # message lengths 0..MAX_LEN
+
+
 def draw(rnd):
-    L = rnd.randrange(0, 201)
+    L = rnd.randrange(0, MAX_LEN + 1)
     m = bytes(rnd.randrange(32, 127) for _ in range(L))
     size = int(10 ** rnd.uniform(0, 9))
     d = rnd.randrange(1, 21)
