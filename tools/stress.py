@@ -51,7 +51,12 @@ def main():
     n_exact = n_prop = 0
     nonces = 0
     fails = []
+    t_report = time.time() + 60
     while time.time() < t_end:
+        if time.time() > t_report:  # progress for long runs (a silent GPU command looks hung)
+            print(f"stress: {n_exact} exact, {n_prop} property, {len(fails)} failures so far", file=sys.stderr,
+                  flush=True)
+            t_report += 60
         m, lo, hi = draw(rnd)
         got = p1_amd.scan(m, lo, hi)
         nonces += hi - lo + 1
