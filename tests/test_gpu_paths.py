@@ -64,6 +64,29 @@ def test_k3_every_layout_vs_oracle(reinit, oracle_mod):
     assert s["fast_nonces"] > 3 * s["generic_nonces"]
 
 
+def test_every_tail_layout_vs_oracle(reinit, oracle_mod):
+    """Exhaustive over the tail layout: every (L + 1) % 64 = r in 0..63 x
+    every digit count d in 1..20, with and without a midstate block, at
+    k = 3 (occupancy floor 1): every variant, PRE/TRAIL, MODEs 5 (whole
+    10^k blocks up to k = 7) and 7, and the generic decades d <= 3, against
+    the oracle."""
+    g = reinit(P1HIP_MIN_FAST_THREADS=1)
+    rnd = random.Random(37)
+    g.reset_stats()
+    for r in range(64):
+        for d in range(1, 21):
+            L = (r - 1) % 64 + 64 * rnd.randrange(0, 2)
+            m = bytes(rnd.randrange(32, 127) for _ in range(L))
+            q = r + d - 1
+            dlo = 0 if d == 1 else 10 ** (d - 1)
+            lo = dlo + rnd.randrange(0, min(10**4, 10**d - dlo))
+            extra = {67: 20000, 68: 200000, 69: 2 * 10**6, 70: 2 * 10**7}.get(q, 0)
+            hi = min(lo + rnd.randrange(3000, 6000) + extra, U64_MAX)
+            assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=16), (L, d, lo, hi)
+    s = g.get_stats()
+    assert s["fast_nonces"] > 3 * s["generic_nonces"]
+
+
 def test_k2_every_layout_vs_oracle(reinit, oracle_mod):
     """Occupancy floor 200 on 30,000-nonce ranges: k = 2 (100 nonces per
     thread) on every layout -- the only way to run <13,1> and the k = 2

@@ -299,3 +299,33 @@ def test_sharded_oracle_equals_serial(oracle_mod):
                 if s:
                     keys.append(oracle_mod.scan("bradfitz", s[0], s[1]))
             assert combine_keys(keys) == oracle_mod.scan("bradfitz", lo, hi)
+
+
+def test_emu_every_tail_layout(oracle_mod):
+    """Exhaustive over the tail layout: every (L + 1) % 64 = r in 0..63 x
+    every digit count d in 4..20 (the layout -- which bytes hold which
+    digit, B_tail, the variant and k -- depends only on r and d), with and
+    without a midstate block, at k = 3 (occupancy floor 1), against the
+    oracle.  MODE 5 with 6 or 7 digits in tail block 1 needs 10^6 / 10^7-
+    aligned blocks, too many for the host replay: those run their ragged
+    edges only (the GPU test runs the blocks)."""
+    import concurrent.futures as cf
+
+    rnd = random.Random(10)
+    cases = []
+    for r in range(64):
+        for d in range(4, 21):
+            L = (r - 1) % 64 + 64 * rnd.randrange(0, 2)
+            m = bytes(rnd.randrange(32, 127) for _ in range(L))
+            q = r + d - 1
+            lo = 10 ** (d - 1) + rnd.randrange(0, 10**4)
+            hi = min(lo + {67: 24999, 68: 219999}.get(q, 4999), U64_MAX)
+            cases.append((m, lo, hi))
+
+    def run(c):
+        m, lo, hi = c
+        return emu(m, lo, hi, minthreads=1)[0] == oracle_mod.scan(m, lo, hi, threads=1), c
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        bad = [c for ok, c in ex.map(run, cases) if not ok]
+    assert not bad, bad[:3]
