@@ -87,6 +87,27 @@ def test_every_tail_layout_vs_oracle(reinit, oracle_mod):
     assert s["fast_nonces"] > 3 * s["generic_nonces"]
 
 
+@pytest.mark.parametrize("k", [1, 2])
+def test_every_tail_layout_small_k_vs_oracle(reinit, oracle_mod, k):
+    """The same exhaustive (r, d) grid at k = 2 and k = 1 (occupancy floor
+    200 on ranges of 3 x 10^(k+2) nonces: the planner lowers k until the
+    decade has 200 threads), where the lo digits and their deltas sit in
+    other bytes and words than at k = 3."""
+    g = reinit(P1HIP_MIN_FAST_THREADS=200)
+    rnd = random.Random(38 + k)
+    g.reset_stats()
+    span = 3 * 10 ** (k + 2)
+    for r in range(64):
+        for d in range(4, 21):
+            L = (r - 1) % 64 + 64 * rnd.randrange(0, 2)
+            m = bytes(rnd.randrange(32, 127) for _ in range(L))
+            lo = 10 ** (d - 1) + rnd.randrange(0, 10**5)
+            hi = lo + span - 1
+            assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=16), (L, d, lo, hi, k)
+    s = g.get_stats()
+    assert s["fast_nonces"] > 3 * s["generic_nonces"]
+
+
 def test_k2_every_layout_vs_oracle(reinit, oracle_mod):
     """Occupancy floor 200 on 30,000-nonce ranges: k = 2 (100 nonces per
     thread) on every layout -- the only way to run <13,1> and the k = 2

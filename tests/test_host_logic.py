@@ -329,3 +329,28 @@ def test_emu_every_tail_layout(oracle_mod):
     with cf.ThreadPoolExecutor(8) as ex:
         bad = [c for ok, c in ex.map(run, cases) if not ok]
     assert not bad, bad[:3]
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_emu_every_tail_layout_small_k(oracle_mod, k):
+    """The exhaustive (r, d) grid at k = 2 and 1 (occupancy floor 200 on
+    ranges of 3 x 10^(k+2) nonces), replayed on the CPU against the oracle."""
+    import concurrent.futures as cf
+
+    rnd = random.Random(11 + k)
+    span = 3 * 10 ** (k + 2)
+    cases = []
+    for r in range(64):
+        for d in range(4, 21):
+            L = (r - 1) % 64 + 64 * rnd.randrange(0, 2)
+            m = bytes(rnd.randrange(32, 127) for _ in range(L))
+            lo = 10 ** (d - 1) + rnd.randrange(0, 10**5)
+            cases.append((m, lo, lo + span - 1))
+
+    def run(c):
+        m, lo, hi = c
+        return emu(m, lo, hi, minthreads=200)[0] == oracle_mod.scan(m, lo, hi, threads=1), c
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        bad = [c for ok, c in ex.map(run, cases) if not ok]
+    assert not bad, bad[:3]
