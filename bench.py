@@ -5,14 +5,21 @@ Metric (BASELINE.json): SHA-256 nonce-hashes/s (GH/s) at 1/2/4/8 MI355X and
 the fraction of the integer-VALU roofline.
 
 Workloads (BASELINE.json configs):
-  c2  configs[1]: msg "bradfitz" (8 B), nonces [0, 2^32) per GPU, one SHA-256
-      compression per nonce.  The default at N = 1 (the metric's config).
-  c3  configs[2]: 120-byte msg (host midstate), [0, 2^34) per GPU, 2 tail blocks.
   c4  configs[3]: msg "bradfitz", the FIXED job [0, 2^38) split contiguously
-      over the N GPUs (strong scaling).  The default at N > 1: north_star's
-      scaling target is stated on this range.
+      over the N GPUs (strong scaling).  The default at EVERY N: north_star's
+      1 -> 8 GPU scaling target is stated on this range, so the N = 1 line
+      and every point of the driver's 1/2/4/8 scaling run time the same job.
+  c2  configs[1]: msg "bradfitz" (8 B), nonces [0, 2^32) per GPU, one SHA-256
+      compression per nonce.
+  c3  configs[2]: 120-byte msg (host midstate), [0, 2^34) per GPU, 2 tail blocks.
+At N = 1 the line also carries c2 and c3 as timed sub-results (`by_config`),
+each checked against its independently pinned answer.
 A step is one full scan of the job (the drop-in for miner.go:56-63) ending
 with the (hash, nonce) result on the host.
+
+Production settings only: the library's test knobs (P1HIP_*, honoured only
+under P1HIP_TEST_KNOBS=1) must be off -- bench.py exits 4 before timing
+anything otherwise, and prints "test_knobs": {} in the line.
 
 How N GPUs are driven:
   * torchrun (WORLD_SIZE > 1, the driver's launch): one process per GPU; each
@@ -42,10 +49,9 @@ sys.path.insert(0, ROOT)
 # x 2.4 GHz max clock.  tools/valu_peak measures the per-instruction rates
 # (profiles/r01_valu_peak.jsonl).
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
-# SURVEY.md 8(d)'s peak assumed 64 int32 lane-ops/clk/CU (39.32 T/s); the
-# measured rates are 2x that for bitop3/add/xor and equal to it for
-# alignbit/add3 (profiles/r01_valu_peak.jsonl), so it is reported beside.
-SURVEY_PEAK_OPS = 39.32e12
+# (SURVEY.md 8(d)'s 39.32 T/s assumed 64 lane-ops/clk/CU; it is superseded by
+# this figure, which tools/valu_peak confirms for add/xor/shift/bitop3 --
+# DESIGN.md 4 "Roofline numbers".)
 ALG_OPS_PER_COMPRESSION = 1384  # 64 rounds x 14 + 48 schedule words x 10 + 8
 # The reference's own published rate for bitcoin.Hash: "around 10,000 per
 # second" on a typical Andrew Linux machine (p1.pdf 4.1).
@@ -106,7 +112,7 @@ def resolve_run(gpus, config, env, visible, force_dist=False):
         if gpus > visible:
             raise UsageError(f"bench.py: --gpus {gpus} but only {visible} GPU(s) are visible")
         mode, n = ("library" if gpus > 1 else "single"), gpus
-    cfg = config or ("c2" if n == 1 else "c4")
+    cfg = config or "c4"  # north_star's scaling job at every N
     return {"mode": mode, "n": n, "rank": rank, "world": world, "local_rank": local, "config": cfg}
 
 
@@ -129,7 +135,10 @@ def known_answer(cfg, n):
     for v in vecs:
         if v.get("large") and bytes.fromhex(v["msg_hex"]) == cfg["msg"] and v["lower"] == 0 \
                 and v["upper"] == total - 1:
-            return (v["hash"], v["nonce"]), v["source"]
+            src = v["source"]
+            if v.get("reference_pinned") is False:
+                src += " [parity-unpinned: no reference-held fixture covers this range]"
+            return (v["hash"], v["nonce"]), src
     return None, None
 
 
@@ -310,6 +319,8 @@ def scaling_report(units, steps, ms_per_step):
              "kernel_GH_s": (u["nonces"] / (k * 1e-3) / 1e9) if k > 0 else None}
         if "ordinal" in u:
             e["ordinal"] = u["ordinal"]
+        if "identity" in u:
+            e["identity"] = u["identity"]
         out.append(e)
     ks = [e["kernel_ms_per_step"] for e in out if e["shard"] is not None]
     rep = {"units": out}
@@ -329,18 +340,213 @@ def scaling_report(units, steps, ms_per_step):
     return rep
 
 
+def rocprof_row(config):
+    """Newest committed rocprofv3 summary of this config's timed k_scan
+    launches (profiles/*_<config>_kernel_stats_workload.csv, the row over the
+    launches after the warm-up ones, tools/summarize_prof.py --skip-launches):
+    (average ns per launch, source) or (None, None)."""
+    import csv
+
+    best = (None, None)
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_kernel_stats_workload.csv"))):
+        with open(p) as f:
+            for row in csv.DictReader(f):
+                if row["Name"].startswith("k_scan (launches after"):
+                    best = (float(row["AverageNs"]), os.path.relpath(p, ROOT))
+    return best
+
+
+class RooflineError(ValueError):
+    pass
+
+
+def check_fracs(roof, b_tail):
+    """No field named frac / frac_* may exceed 1 for a 1-block config: a
+    fraction of the peak above 1 would say the timed kernel is not doing the
+    work it is charged with (VERDICT r03 weak #3).  Raises RooflineError."""
+    if b_tail != 1:
+        return
+    stack = [("roofline", roof)]
+    while stack:
+        path, d = stack.pop()
+        for k, v in d.items():
+            if isinstance(v, dict):
+                stack.append((f"{path}.{k}", v))
+            elif (k == "frac" or k.startswith("frac_")) and isinstance(v, (int, float)) and v > 1.0:
+                raise RooflineError(f"{path}.{k} = {v:.4f} > 1 on a 1-block config")
+
+
+def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof=(None, None), single_gpu=True):
+    """The bench line's `roofline` block for the dominant kernel k_scan.
+
+    achieved = algorithmic ops (1384 x B_tail per nonce, SURVEY.md 8(d)) /
+    the HIP-event duration of the launches (stats: scan_alg_ops,
+    scan_kernel_ms, scan_launches, scan_nonces summed over this process's
+    devices); peak = 78.64 T int32 lane-ops/s.  Beside it: frac_rocprof (the
+    same ops over the committed rocprofv3 average of this config's timed
+    launches, single GPU only), the executed-instruction fraction from the
+    PMC summary, and the loop-mix issue fraction."""
+    k_ms = stats["scan_kernel_ms"]
+    k_n = stats["scan_launches"]
+    achieved = stats["scan_alg_ops"] / (k_ms * 1e-3) if k_ms > 0 else 0.0
+    k_rate = stats["scan_nonces"] / (k_ms * 1e-3) if k_ms > 0 else 0.0  # nonces/s per device
+    roof = {
+        "bound": "valu-int32",
+        "achieved": achieved / 1e12,
+        "peak": VALU_PEAK_OPS / 1e12,
+        "unit": "TOP/s",
+        "frac": achieved / VALU_PEAK_OPS,
+        "peak_basis": "256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md; tools/valu_peak); "
+                      "supersedes SURVEY.md 8(d)'s 39.32 T",
+        "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+        "traffic_unit": "bytes/launch (PMC FETCH_SIZE+WRITE_SIZE)",
+        "traffic_source": pmc_src,
+        "kernel": "k_scan (one launch per scan covers every decade; algorithmic ops = 1384 x B_tail per nonce)",
+        "alg_ops_per_nonce": ALG_OPS_PER_COMPRESSION * cfg["b_tail"],
+        "avg_launch_ms": k_ms / k_n if k_n else None,
+        "launches_per_step": k_n / steps if steps else None,
+        "kernel_hashes_per_s_G": k_rate / 1e9,
+        "fast_nonce_share": stats["fast_nonces"] / max(1, stats["fast_nonces"] + stats["generic_nonces"]),
+    }
+    avg_ns, src = rocprof
+    if single_gpu and avg_ns and k_n:
+        # one launch of this config's plan; rocprofv3 --kernel-trace average
+        # of the same command's timed launches
+        roof["frac_rocprof"] = stats["scan_alg_ops"] / k_n / (avg_ns * 1e-9) / VALU_PEAK_OPS
+        roof["rocprof_avg_launch_ms"] = avg_ns / 1e6
+        roof["rocprof_source"] = src
+    if pmc and pmc.get("valu_wave_instr_per_nonce"):
+        # SURVEY.md 8(d) accounting rule: the executed-instruction fraction
+        # SQ_INSTS_VALU x 64 / (t x peak), this run's kernel rate x the PMC
+        # instructions per nonce
+        ipn = pmc["valu_wave_instr_per_nonce"]
+        ex = {
+            "valu_instr_per_nonce": ipn,
+            "achieved": ipn * k_rate / 1e12,
+            "frac": ipn * k_rate / VALU_PEAK_OPS,
+            "simd_cycles_per_valu_wave_instr": pmc.get("simd_cycles_per_valu_wave_instr"),
+            "effective_clock_GHz": pmc.get("effective_clock_GHz"),
+            "source": pmc_src,
+            "note": "frac counts executed VALU lane-instructions against the same 78.6 T peak "
+                    "(SURVEY.md 8(d) accounting rule)",
+        }
+        msg = cfg["msg"]
+        mix_ab = workload_mix(len(msg), 0, job_total(cfg, 1) - 1)
+        if mix_ab and k_rate > 0:
+            # the executed loop mix at its ideal issue rate vs the SIMD
+            # cycles this run spent per wave-iteration (64 nonces)
+            clk = (pmc.get("effective_clock_GHz") or 2.4) * 1e9
+            spent = 1024 * clk * 64 / k_rate
+            ideal = mix_ab[0] * IDEAL_COST_A + mix_ab[1] * IDEAL_COST_B
+            ex["mix_issue_frac"] = ideal / spent
+            ex["loop_mix_per_nonce"] = {"half_rate_A": mix_ab[0], "full_rate_B": mix_ab[1],
+                                        "source": VARIANT_PROFILE}
+            ex["mix_issue_note"] = ("ideal SIMD cycles of the loop mix (A x 4.23 + B x 2.13, the fastest "
+                                    "single-class issue costs measured by tools/valu_runs) / SIMD cycles spent "
+                                    "per 64 nonces")
+        roof["executed"] = ex
+    if cfg["b_tail"] != 1:
+        # the algorithmic count charges both tail blocks per nonce; the kernel
+        # compresses the hi-digit block once per 10^k nonces and reads the
+        # lo-only block's schedule from a table (MODE 5): the algorithmic
+        # rate is not a utilisation, so it is not called a fraction here
+        roof["alg_ops_over_peak"] = roof.pop("frac")
+        roof["frac"] = roof.get("executed", {}).get("frac")
+        roof["frac_basis"] = ("executed VALU lane-instructions (PMC) / peak: for this 2-block config the "
+                              "algorithmic count overstates the work (block 0 once per 10^k nonces, block 1's "
+                              "schedule tabulated), see alg_ops_over_peak")
+        if "frac_rocprof" in roof:
+            roof["alg_ops_over_peak_rocprof"] = roof.pop("frac_rocprof")
+    mix = mix_roofline()
+    if mix and k_ms > 0:
+        mix["peak_GH_s"] = mix["peak_GH_s_per_block"] / cfg["b_tail"]
+        mix["speed_vs_unhoisted_mix"] = k_rate / 1e9 / mix["peak_GH_s"]
+        mix["note"] = ("kernel rate / the rate the FULL algorithmic compression would reach with every "
+                       "instruction at its own measured peak: a speed ratio, not a utilisation (the kernel "
+                       "hoists per-thread rounds and schedule words, so it can exceed 1)")
+        roof["unhoisted_mix"] = mix
+    check_fracs(roof, cfg["b_tail"])
+    return roof
+
+
+def device_identity(index):
+    """Ordinal, PCI bus id, UUID, arch and host of a device the library
+    opened (p1hip_device_info), for the per-GPU records."""
+    import socket
+
+    import p1_amd
+
+    info = p1_amd.device_info(index)
+    return {"hostname": socket.gethostname(), "ordinal": info["ordinal"], "pci_bus_id": info["pci_bus_id"],
+            "uuid": info["uuid"], "arch": info["arch"], "cu_count": info["cu_count"]}
+
+
+def timed_steps(step, steps, warmup, barrier):
+    """W untimed steps, then K timed ones bracketed by barrier() (a
+    torch.distributed barrier + device synchronise); library stats reset and
+    HIP-event profiling on over exactly the timed steps."""
+    import p1_amd
+
+    for _ in range(warmup):
+        step()
+    p1_amd.reset_stats()
+    p1_amd.set_profiling(True)
+    barrier()
+    t0 = time.perf_counter()
+    results, marks = [], [t0]
+    for _ in range(steps):
+        results.append(step())  # synchronous: the (hash, nonce) result is on the host
+        marks.append(time.perf_counter())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    p1_amd.set_profiling(False)
+    step_ms = sorted((b - a) * 1e3 for a, b in zip(marks, marks[1:]))
+    return elapsed, step_ms, results, p1_amd.get_stats()
+
+
+# by_config sub-results of the N = 1 line: (config, warmup, steps)
+SUB_CONFIGS = [("c2", 2, 5), ("c3", 1, 3)]
+
+
+def sub_result(name, warmup, steps, sync):
+    """One other BASELINE config timed on the same device after the headline
+    run: value, ms_per_step, the roofline fraction and the check against its
+    independently pinned answer."""
+    import p1_amd
+
+    cfg = CONFIGS[name]
+    total = job_total(cfg, 1)
+    elapsed, step_ms, results, stats = timed_steps(lambda: p1_amd.scan(cfg["msg"], 0, total - 1), steps, warmup,
+                                                   sync)
+    pmc, pmc_src = pmc_summary(name)
+    roof = assemble_roofline(name, cfg, stats, steps, pmc, pmc_src, rocprof_row(name))
+    known, src = known_answer(cfg, 1)
+    res = results[-1]
+    out = {"workload": cfg["desc"], "value": total * steps / elapsed / 1e9, "unit": "GH/s",
+           "steps": steps, "warmup": warmup, "ms_per_step": elapsed * 1e3 / steps,
+           "kernel_hashes_per_s_G": roof["kernel_hashes_per_s_G"], "avg_launch_ms": roof["avg_launch_ms"],
+           "frac": roof["frac"], "result": list(res), "consistent": all(r == res for r in results),
+           "matches_known": (tuple(res) == tuple(known)) if known else None, "known_source": src}
+    for k in ("frac_rocprof", "alg_ops_over_peak", "frac_basis"):
+        if k in roof:
+            out[k] = roof[k]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
-                    help="default: c2 at one GPU, c4 (fixed [0,2^38) job) at N > 1")
+                    help="default: c4 (configs[3], the fixed [0,2^38) job) at every N")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-small-request", action="store_true",
                     help="skip the configs[0]-sized latency probe (profiling runs: keeps every "
                          "k_scan launch in the rocprof summary a workload launch)")
+    ap.add_argument("--no-by-config", action="store_true",
+                    help="skip the c2/c3 sub-results of the N = 1 line (profiling runs)")
     ap.add_argument("--dist", action="store_true",
                     help="take the one-process-per-GPU torch.distributed path even when WORLD_SIZE is 1 "
                          "(rehearses the driver's N>1 launch, RCCL included, on one GPU)")
@@ -348,6 +554,17 @@ def main():
                     help="torchrun path: nccl = RCCL over xGMI (production); gloo only to rehearse "
                          "several ranks on one GPU")
     args = ap.parse_args()
+
+    import p1_amd
+    from p1_amd.build import ensure_built
+
+    ensure_built()
+    # production settings only: refuse before any device is touched
+    knobs = p1_amd.test_knobs()
+    if knobs:
+        print(f"bench.py: refusing to time with library test knobs in force: {knobs} "
+              f"(unset P1HIP_TEST_KNOBS)", file=sys.stderr)
+        sys.exit(4)
 
     import torch
 
@@ -363,11 +580,7 @@ def main():
 
     import torch.distributed as dist
 
-    import p1_amd
-    from p1_amd.build import ensure_built
     from p1_amd.dist import distributed_scan
-
-    ensure_built()
 
     msg = cfg["msg"]
     total = job_total(cfg, n_gpus)
@@ -409,22 +622,10 @@ def main():
     for _ in range(args.warmup):
         step()
     timing.clear()
-    p1_amd.reset_stats()
-    p1_amd.set_profiling(True)
-    barrier()
-    t0 = time.perf_counter()
-    results, marks = [], [t0]
-    for _ in range(args.steps):
-        results.append(step())  # synchronous: the (hash, nonce) result is on the host
-        marks.append(time.perf_counter())
-    barrier()
-    elapsed = time.perf_counter() - t0
-    step_ms = sorted((b - a) * 1e3 for a, b in zip(marks, marks[1:]))
-    p1_amd.set_profiling(False)
-    stats = p1_amd.get_stats()
+    elapsed, step_ms, results, stats = timed_steps(step, args.steps, 0, barrier)
 
     if mode == "torchrun":
-        from p1_amd.dist import gather_rank_stats
+        from p1_amd.dist import gather_rank_identity, gather_rank_stats
 
         shard = timing.get("shard")
         units = gather_rank_stats({
@@ -433,18 +634,28 @@ def main():
             "kernel_ms": stats["scan_kernel_ms"], "scan_ms": timing.get("scan_s", 0.0) * 1e3,
             "gather_ms": timing.get("gather_s", 0.0) * 1e3, "elapsed_ms": elapsed * 1e3,
             "step_ms_median": statistics.median(step_ms) if step_ms else 0.0}, device=coll_dev)
+        idents = gather_rank_identity(dict(device_identity(0), rank=rank), device=coll_dev)
+        for u, ident in zip(units, idents):
+            u["identity"] = ident
         elapsed = max(u["elapsed_ms"] for u in units) / 1e3  # max over ranks
+        topology = {"launch": "torchrun", "backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                    "ranks_in_gather": len(idents)}
     else:
         units = []
         for i in range(len(devices)):
             ds = p1_amd.get_device_stats(i)
-            units.append({"device": i, "ordinal": ds["ordinal"],
+            units.append({"device": i, "ordinal": ds["ordinal"], "identity": device_identity(i),
                           "shard_lo": ds["shard_first"], "shard_hi": ds["shard_last"] if ds["active"] else 0,
                           "nonces": ds["scan_nonces"], "launches": ds["scan_launches"],
                           "alg_ops": ds["scan_alg_ops"], "kernel_ms": ds["scan_kernel_ms"],
                           "scan_ms": ds["phase1_ms"], "gather_ms": ds["gather_ms"]})
             if not ds["active"]:
                 units[-1]["shard_lo"] = 1
+        topology = {"launch": mode, "backend": "rccl (ncclCommInitAll in libp1hip)" if n_gpus > 1 else None,
+                    "world_size": 1, "ranks_in_gather": None}
+    gpus_seen = {(u["identity"]["hostname"], u["identity"]["pci_bus_id"], u["identity"]["uuid"]) for u in units}
+    topology["distinct_gpus"] = len(gpus_seen)
+    topology["hosts"] = sorted({h for h, _, _ in gpus_seen})
 
     result = results[-1]
     consistent = all(r == result for r in results)
@@ -454,68 +665,9 @@ def main():
         hashes = total * args.steps
         value = hashes / elapsed / 1e9
         ms_per_step = elapsed * 1e3 / args.steps
-        k_ms = stats["scan_kernel_ms"]  # summed over this process's devices
-        k_n = stats["scan_launches"]
-        # one launch = one device's k_scan; its algorithmic ops / its own duration
-        achieved = stats["scan_alg_ops"] / (k_ms * 1e-3) if k_ms > 0 else 0.0
-        k_rate = stats["scan_nonces"] / (k_ms * 1e-3) if k_ms > 0 else 0.0  # nonces/s per device
         pmc, pmc_src = pmc_summary(run["config"])
-        roofline = {
-            "bound": "valu-int32",
-            "achieved": achieved / 1e12,
-            "peak": VALU_PEAK_OPS / 1e12,
-            "unit": "TOP/s",
-            "frac": achieved / VALU_PEAK_OPS,
-            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
-            "traffic_unit": "bytes/launch (PMC FETCH_SIZE+WRITE_SIZE)",
-            "traffic_source": pmc_src,
-            "kernel": "k_scan (one launch per scan covers every decade; algorithmic ops = 1384 x B_tail per nonce)",
-            "alg_ops_per_nonce": ALG_OPS_PER_COMPRESSION * cfg["b_tail"],
-            "avg_launch_ms": k_ms / k_n if k_n else None,
-            "launches_per_step": k_n / args.steps,
-            "kernel_hashes_per_s_G": k_rate / 1e9,
-            "frac_vs_survey_peak": achieved / SURVEY_PEAK_OPS,
-            "fast_nonce_share": stats["fast_nonces"] / max(1, stats["fast_nonces"] + stats["generic_nonces"]),
-        }
-        if pmc and pmc.get("valu_wave_instr_per_nonce"):
-            # SURVEY.md 8(d) accounting rule: beside the algorithmic fraction,
-            # the executed-instruction fraction SQ_INSTS_VALU x 64 / (t x peak),
-            # with this run's kernel rate and the PMC instructions per nonce
-            ipn = pmc["valu_wave_instr_per_nonce"]
-            roofline["executed"] = {
-                "valu_instr_per_nonce": ipn,
-                "achieved": ipn * k_rate / 1e12,
-                "frac": ipn * k_rate / VALU_PEAK_OPS,
-                "simd_cycles_per_valu_wave_instr": pmc.get("simd_cycles_per_valu_wave_instr"),
-                "effective_clock_GHz": pmc.get("effective_clock_GHz"),
-                "source": pmc_src,
-                "note": "frac counts executed VALU lane-instructions against the same 78.6 T peak "
-                        "(SURVEY.md 8(d) accounting rule)",
-            }
-            mix_ab = workload_mix(len(msg), 0, total - 1)
-            if mix_ab and k_rate > 0:
-                # the executed loop mix at its ideal issue rate vs the SIMD
-                # cycles this run spent per wave-iteration (64 nonces)
-                clk = (pmc.get("effective_clock_GHz") or 2.4) * 1e9
-                spent = 1024 * clk * 64 / k_rate
-                ideal = mix_ab[0] * IDEAL_COST_A + mix_ab[1] * IDEAL_COST_B
-                roofline["executed"]["mix_issue_frac"] = ideal / spent
-                roofline["executed"]["loop_mix_per_nonce"] = {"half_rate_A": mix_ab[0], "full_rate_B": mix_ab[1],
-                                                              "source": VARIANT_PROFILE}
-                roofline["executed"]["mix_issue_note"] = (
-                    "ideal SIMD cycles of the loop mix (A x 4.23 + B x 2.13, the fastest single-class "
-                    "issue costs measured by tools/valu_runs) / SIMD cycles spent per 64 nonces")
-            if roofline["frac"] > 1.0:
-                roofline["executed"]["why_alg_frac_above_1"] = (
-                    "the algorithmic count charges both tail blocks per nonce (SURVEY.md 8(d)); the kernel "
-                    "compresses the hi-digit block once per 10^k nonces (PRE) and, where the second block "
-                    "holds only lo digits (MODE 5), reads that block's whole message schedule from a "
-                    "per-launch table, so per nonce it executes the 64 rounds of one block and no schedule")
-        mix = mix_roofline()
-        if mix and k_ms > 0:
-            mix["peak_GH_s"] = mix["peak_GH_s_per_block"] / cfg["b_tail"]
-            mix["frac"] = k_rate / 1e9 / mix["peak_GH_s"]
-            roofline["mix_roofline"] = mix
+        roofline = assemble_roofline(run["config"], cfg, stats, args.steps, pmc, pmc_src, rocprof_row(run["config"]),
+                                     single_gpu=(n_gpus == 1))
         parallelism = {"single": "1 GPU",
                        "library": f"cost-balanced contiguous range-shard x{n_gpus} (p1hip_plan_shards), one process (p1hip_init({n_gpus}): thread per device, "
                                   f"ncclCommInitAll + ncclAllGather of 16-B partials)",
@@ -554,12 +706,25 @@ def main():
                 "launch": mode,
                 "devices": devices if mode != "torchrun" else f"one per rank, {world} ranks",
             },
+            "test_knobs": knobs,
+            "library": {"path": os.path.relpath(p1_amd.lib_path(), ROOT), "version": p1_amd.version()},
+            "topology": topology,
             "roofline": roofline,
             "per_gpu": scaling_report(units, args.steps, ms_per_step),
             "result": {"hash": result[0], "nonce": result[1], "consistent": consistent,
                        "matches_known": (tuple(result) == tuple(known)) if known else None,
                        "known": list(known) if known else None, "known_source": known_src},
         }
+        if n_gpus == 1 and mode != "torchrun" and not args.no_by_config:
+            # the other BASELINE configs on the same GPU, after the timed
+            # headline run (never inside it)
+            line["by_config"] = {run["config"]: {"value": value, "ms_per_step": ms_per_step,
+                                                 "frac": roofline.get("frac"),
+                                                 "matches_known": line["result"]["matches_known"],
+                                                 "headline": True}}
+            for name, w, k in SUB_CONFIGS:
+                if name != run["config"]:
+                    line["by_config"][name] = sub_result(name, w, k, barrier)
         # configs[0]'s request (client 'bradfitz' maxNonce 9999) as one
         # drop-in call: per-request latency of p1hip_scan on a small job
         lat = []
@@ -575,11 +740,14 @@ def main():
         if n_gpus == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(msg, 1 << 31, args.cpu_seconds)
         print(json.dumps(line), flush=True)
+        wrong = [k for k, v in line.get("by_config", {}).items() if v.get("matches_known") is False]
+    else:
+        wrong = []
 
     if mode == "torchrun":
         dist.destroy_process_group()
     p1_amd.shutdown()
-    if known and tuple(result) != tuple(known):
+    if (known and tuple(result) != tuple(known)) or wrong:
         sys.exit(3)  # a wrong answer is not a benchmark result
 
 

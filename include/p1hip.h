@@ -105,7 +105,6 @@ typedef struct {
   uint64_t fast_launches;    /* fast segments (one thread per 10^k nonces)        */
   uint64_t fast_nonces;      /* nonces hashed by fast segments                    */
   uint64_t fast_alg_ops;     /* algorithmic int32 ops: 1384 * B_tail per nonce    */
-  double fast_kernel_ms;     /* unused (0), kept for layout stability             */
   uint64_t generic_launches; /* generic segments (one thread per nonce)           */
   uint64_t generic_nonces;   /* nonces hashed by generic segments                 */
   double scan_wall_ms;       /* host wall time inside p1hip_scan                  */
@@ -151,8 +150,33 @@ void p1hip_reset_stats(void);
 /* Number of devices currently in use (0 before init). */
 int p1hip_device_count(void);
 
+/* Identity of device `index` (as for p1hip_get_device_stats), so a record of
+ * an N-GPU run can show that N distinct GPUs took part. */
+typedef struct {
+  int32_t ordinal;           /* HIP device ordinal                                */
+  int32_t cu_count;          /* compute units                                     */
+  int32_t clock_khz;         /* peak engine clock                                 */
+  int32_t reserved;
+  uint64_t hbm_bytes;        /* device memory                                     */
+  char pci_bus_id[32];       /* "dddd:bb:dd.f" (hipDeviceGetPCIBusId)             */
+  char arch[32];             /* gcnArchName, e.g. "gfx950:sramecc+:xnack-"        */
+  unsigned char uuid[16];    /* hipDeviceProp_t.uuid                              */
+} p1hip_device_info_t;
+
+int p1hip_device_info(int index, p1hip_device_info_t *out);
+
 const char *p1hip_last_error(void);
 const char *p1hip_version(void);
+
+/* Test-only knobs in force for this process.  The library honours its
+ * P1HIP_* test knobs (occupancy floor, injected failures, table and launch
+ * caps, combine mode ...) only while the master switch P1HIP_TEST_KNOBS=1 is
+ * set in the environment; otherwise they are ignored and this returns "".
+ * With the switch set it returns "P1HIP_TEST_KNOBS=1" followed by
+ * ";NAME=value" for every knob that is set.  bench.py refuses to time a run
+ * for which this is not "".  The string is per thread and valid until the
+ * next call from that thread. */
+const char *p1hip_test_knobs(void);
 
 /* Release streams, buffers and communicators.  Safe to call twice. */
 void p1hip_shutdown(void);

@@ -22,6 +22,8 @@ from ._lib import (  # noqa: F401
     get_device_stats,
     reset_stats,
     device_count,
+    device_info,
+    test_knobs,
     shutdown,
     version,
 )

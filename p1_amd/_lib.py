@@ -24,7 +24,6 @@ class Stats(ctypes.Structure):
         ("fast_launches", U64),
         ("fast_nonces", U64),
         ("fast_alg_ops", U64),
-        ("fast_kernel_ms", ctypes.c_double),
         ("generic_launches", U64),
         ("generic_nonces", U64),
         ("scan_wall_ms", ctypes.c_double),
@@ -59,6 +58,24 @@ class DeviceStats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class DeviceInfo(ctypes.Structure):
+    _fields_ = [
+        ("ordinal", ctypes.c_int32),
+        ("cu_count", ctypes.c_int32),
+        ("clock_khz", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("hbm_bytes", U64),
+        ("pci_bus_id", ctypes.c_char * 32),
+        ("arch", ctypes.c_char * 32),
+        ("uuid", ctypes.c_ubyte * 16),
+    ]
+
+    def as_dict(self):
+        return {"ordinal": self.ordinal, "cu_count": self.cu_count, "clock_khz": self.clock_khz,
+                "hbm_bytes": self.hbm_bytes, "pci_bus_id": self.pci_bus_id.decode(errors="replace"),
+                "arch": self.arch.decode(errors="replace"), "uuid": bytes(self.uuid).hex()}
+
+
 def lib_path():
     # P1HIP_LIB selects an alternative build of the same library (A/B tuning
     # builds under p1_amd/variants/); default is the in-tree libp1hip.so.
@@ -81,6 +98,8 @@ SIGNATURES = [
     ("p1hip_reset_stats", None, []),
     ("p1hip_get_device_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(DeviceStats)]),
     ("p1hip_device_count", ctypes.c_int, []),
+    ("p1hip_device_info", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(DeviceInfo)]),
+    ("p1hip_test_knobs", ctypes.c_char_p, []),
     ("p1hip_last_error", ctypes.c_char_p, []),
     ("p1hip_version", ctypes.c_char_p, []),
     ("p1hip_shutdown", None, []),
@@ -177,6 +196,21 @@ def get_device_stats(index):
     s = DeviceStats()
     _check(load().p1hip_get_device_stats(int(index), ctypes.byref(s)))
     return s.as_dict()
+
+
+def device_info(index):
+    """Identity of device `index` (p1hip_device_info): ordinal, PCI bus id,
+    arch, CU count, clock, HBM bytes, UUID."""
+    s = DeviceInfo()
+    _check(load().p1hip_device_info(int(index), ctypes.byref(s)))
+    return s.as_dict()
+
+
+def test_knobs():
+    """The library's test knobs in force for this process, as a dict ({} in
+    production: the knobs are honoured only under P1HIP_TEST_KNOBS=1)."""
+    raw = load().p1hip_test_knobs().decode()
+    return dict(kv.split("=", 1) for kv in raw.split(";") if kv)
 
 
 def reset_stats():

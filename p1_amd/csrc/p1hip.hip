@@ -95,8 +95,29 @@ constexpr uint32_t kMaxLaunchBlocks = 1u << 22;
 // P1HIP_SMALL_MAX_NONCES (tests only, read per scan): ranges of at most this
 // many nonces take the one-launch small path (default kSmallMaxNonces; 0
 // turns it off so small parity ranges exercise the fast kernel variants).
+// Every P1HIP_* test knob is read through test_knob(): it is honoured only
+// while the master switch P1HIP_TEST_KNOBS=1 is set (the test fixtures set
+// it), so a stray knob in a production miner's environment changes nothing.
+// p1hip_test_knobs() lists the knobs in force, for bench.py to refuse.
+const char* const kTestKnobs[] = {
+    "P1HIP_SMALL_MAX_NONCES", "P1HIP_MAX_LAUNCH_BLOCKS", "P1HIP_MAX_SCAN_SPAN", "P1HIP_KWTAB_MAX_BYTES",
+    "P1HIP_NO_RCCL",          "P1HIP_FORCE_RCCL",        "P1HIP_MIN_FAST_THREADS", "P1HIP_TEST_FAIL_DEVICE",
+    "P1HIP_NO_TABLE",         "P1HIP_NO_SPLIT",
+};
+
+bool test_knobs_on() {
+  const char* m = getenv("P1HIP_TEST_KNOBS");
+  return m && m[0] == '1' && m[1] == 0;
+}
+
+const char* test_knob(const char* name) {
+  if (!test_knobs_on()) return nullptr;
+  const char* v = getenv(name);
+  return v && *v ? v : nullptr;
+}
+
 uint64_t small_limit() {
-  const char* v = getenv("P1HIP_SMALL_MAX_NONCES");
+  const char* v = test_knob("P1HIP_SMALL_MAX_NONCES");
   if (!v || !*v) return kSmallMaxNonces;
   const uint64_t n = strtoull(v, nullptr, 10);
   return n < kSmallMaxNonces ? n : kSmallMaxNonces;
@@ -107,7 +128,7 @@ uint64_t small_limit() {
 // piece larger than the cap gets a launch of its own (a piece is at most
 // kMaxFastThreads / kBlock = 2^18 workgroups, far below HIP's grid limit).
 uint64_t launch_block_limit() {
-  const char* v = getenv("P1HIP_MAX_LAUNCH_BLOCKS");
+  const char* v = test_knob("P1HIP_MAX_LAUNCH_BLOCKS");
   const uint64_t n = v && *v ? strtoull(v, nullptr, 10) : 0;
   if (n == 0 || n >= kMaxLaunchBlocks) return kMaxLaunchBlocks;
   return n;
@@ -143,7 +164,6 @@ struct Dev {
   uint64_t range_id = 0;        // run_range calls on this device
   // per-scan accounting filled by run_range
   uint64_t fast_launches = 0, fast_nonces = 0, fast_ops = 0, gen_launches = 0, gen_nonces = 0;
-  double fast_ms = 0.0;
   uint64_t scan_launches = 0, scan_nonces = 0, scan_ops = 0;
   double scan_ms = 0.0;
   uint64_t replans = 0;         // shares re-planned without MODE 5 (this scan)
@@ -158,7 +178,7 @@ struct Runtime {
   bool use_rccl = true;   // multi-device combine through ncclAllGather
   bool rccl_one = false;  // P1HIP_FORCE_RCCL=1: communicator even for one device
   // Test-only knobs, read from the environment at init (never set in
-  // production; see tests/test_gpu_parity.py):
+  // production; honoured only under P1HIP_TEST_KNOBS=1, see test_knob):
   //   P1HIP_MIN_FAST_THREADS  planner occupancy floor (1 keeps k = 3 on small
   //                           ranges so every k = 3 variant runs on the GPU)
   //   P1HIP_TEST_FAIL_DEVICE  device index whose scan phase reports a failure
@@ -268,18 +288,18 @@ int init_devs(Runtime& R, const std::vector<int>& ords) {
   // P1HIP_NO_RCCL=1 (tests only): combine the per-device results through the
   // host instead of RCCL, so the multi-device code path (threads, sharding,
   // combine) can be exercised with the same GPU listed twice on a 1-GPU box.
-  const char* norccl = getenv("P1HIP_NO_RCCL");
+  const char* norccl = test_knob("P1HIP_NO_RCCL");
   R.use_rccl = !(norccl && norccl[0] == '1');
-  const char* force = getenv("P1HIP_FORCE_RCCL");
+  const char* force = test_knob("P1HIP_FORCE_RCCL");
   R.rccl_one = force && force[0] == '1' && R.use_rccl;
-  const char* mft = getenv("P1HIP_MIN_FAST_THREADS");
-  R.min_fast_threads = mft && *mft ? strtoull(mft, nullptr, 10) : kMinFastThreads;
-  const char* nsp = getenv("P1HIP_NO_SPLIT");
+  const char* mft = test_knob("P1HIP_MIN_FAST_THREADS");
+  R.min_fast_threads = mft ? strtoull(mft, nullptr, 10) : kMinFastThreads;
+  const char* nsp = test_knob("P1HIP_NO_SPLIT");
   R.split = !(nsp && nsp[0] == '1');
-  const char* ntb = getenv("P1HIP_NO_TABLE");
+  const char* ntb = test_knob("P1HIP_NO_TABLE");
   R.tabulate = !(ntb && ntb[0] == '1');
-  const char* fdev = getenv("P1HIP_TEST_FAIL_DEVICE");
-  R.fail_device = fdev && *fdev ? atoi(fdev) : -1;
+  const char* fdev = test_knob("P1HIP_TEST_FAIL_DEVICE");
+  R.fail_device = fdev ? atoi(fdev) : -1;
   if ((nd > 1 || R.rccl_one) && R.use_rccl) {
     std::vector<ncclComm_t> comms(nd);
     NCCLCHK(ncclCommInitAll(comms.data(), nd, ords.data()));
@@ -311,7 +331,7 @@ int run_small(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
   HIPCHK(hipSetDevice(d.ordinal));
   d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
   d.scan_launches = d.scan_nonces = d.scan_ops = 0;
-  d.fast_ms = d.scan_ms = 0.0;
+  d.scan_ms = 0.0;
   Plan plan;
   std::string err = make_plan(msg, len, lo, hi, plan, false);
   if (!err.empty()) return fail(P1HIP_ERR_ARGS, "planner: " + err);
@@ -382,8 +402,8 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
   }
   const size_t need = (size_t)pow10u(L.tabk) * 64u * sizeof(uint32_t);
   // P1HIP_KWTAB_MAX_BYTES (tests only): a lower cap, to exercise the re-plan
-  const char* capv = getenv("P1HIP_KWTAB_MAX_BYTES");
-  const size_t cap = capv && *capv ? (size_t)strtoull(capv, nullptr, 10) : kMaxKwTabBytes;
+  const char* capv = test_knob("P1HIP_KWTAB_MAX_BYTES");
+  const size_t cap = capv ? (size_t)strtoull(capv, nullptr, 10) : kMaxKwTabBytes;
   if (need > cap) return kNoTable;
   for (;;) {
     size_t held = 0;
@@ -434,7 +454,7 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
   d.range_id++;  // tables referenced from here on are pinned until the next call
   d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
   d.scan_launches = d.scan_nonces = d.scan_ops = 0;
-  d.fast_ms = d.scan_ms = 0.0;
+  d.scan_ms = 0.0;
   Plan plan;
   // plan -> every MODE 5 table -> launches: a table that cannot be had makes
   // the share re-plan without MODE 5 here, before any k_scan of it (or any
@@ -582,13 +602,13 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
 constexpr uint64_t kMaxScanSpan = 1ull << 40;
 int run_share(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, const Runtime& R) {
   // P1HIP_MAX_SCAN_SPAN (tests only, read per scan): smaller pieces
-  const char* sv = getenv("P1HIP_MAX_SCAN_SPAN");
-  const uint64_t span = sv && *sv && strtoull(sv, nullptr, 10) > 0 ? strtoull(sv, nullptr, 10) : kMaxScanSpan;
+  const char* sv = test_knob("P1HIP_MAX_SCAN_SPAN");
+  const uint64_t span = sv && strtoull(sv, nullptr, 10) > 0 ? strtoull(sv, nullptr, 10) : kMaxScanSpan;
   if (hi - lo < span)
     return run_range(d, msg, len, lo, hi, R.profiling, R.min_fast_threads, R.split, R.tabulate);
   Key best = {~0ull, ~0ull};
   uint64_t fl = 0, fn = 0, fo = 0, gl = 0, gn = 0, sl = 0, sn = 0, so = 0;
-  double fms = 0.0, sms = 0.0;
+  double sms = 0.0;
   for (uint64_t a = lo;;) {
     const uint64_t b = hi - a < span ? hi : a + (span - 1);
     int r = run_range(d, msg, len, a, b, R.profiling, R.min_fast_threads, R.split, R.tabulate);
@@ -598,12 +618,12 @@ int run_share(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
     HIPCHK(hipStreamSynchronize(d.stream));
     if (key_lt(k, best)) best = k;
     fl += d.fast_launches; fn += d.fast_nonces; fo += d.fast_ops; gl += d.gen_launches; gn += d.gen_nonces;
-    sl += d.scan_launches; sn += d.scan_nonces; so += d.scan_ops; fms += d.fast_ms; sms += d.scan_ms;
+    sl += d.scan_launches; sn += d.scan_nonces; so += d.scan_ops; sms += d.scan_ms;
     if (b == hi) break;
     a = b + 1;
   }
   d.fast_launches = fl; d.fast_nonces = fn; d.fast_ops = fo; d.gen_launches = gl; d.gen_nonces = gn;
-  d.scan_launches = sl; d.scan_nonces = sn; d.scan_ops = so; d.fast_ms = fms; d.scan_ms = sms;
+  d.scan_launches = sl; d.scan_nonces = sn; d.scan_ops = so; d.scan_ms = sms;
   HIPCHK(hipMemcpyAsync(d.d_res, &best, sizeof(Key), hipMemcpyHostToDevice, d.stream));
   HIPCHK(hipStreamSynchronize(d.stream));  // `best` lives on this stack frame
   return P1HIP_OK;
@@ -730,7 +750,7 @@ int scan_locked(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t upp
       // must not re-report its previous scan)
       d.fast_launches = d.fast_nonces = d.fast_ops = d.gen_launches = d.gen_nonces = 0;
       d.scan_launches = d.scan_nonces = d.scan_ops = 0;
-      d.fast_ms = d.scan_ms = 0.0;
+      d.scan_ms = 0.0;
       d.replans = 0;
       d.small_used = false;
       d.acc.shard_first = slo[i];
@@ -761,11 +781,22 @@ int scan_locked(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t upp
       }
       if (!r && hipStreamSynchronize(d.stream) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipStreamSynchronize");
       } catch (const std::exception& ex) {
-        r = fail(P1HIP_ERR_HIP, std::string("host: ") + ex.what());
+        try {
+          r = fail(P1HIP_ERR_HIP, std::string("host: ") + ex.what());
+        } catch (...) {
+          r = P1HIP_ERR_HIP;
+        }
+      } catch (...) {
+        r = P1HIP_ERR_HIP;
       }
       d.acc.phase1_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - p0).count();
       rcs[i] = r;
-      if (r) errs[i] = g_err;
+      if (r) {
+        try {
+          errs[i] = g_err;
+        } catch (...) {  // the copy allocates; rcs[i] already says what matters
+        }
+      }
     });
     if ((rc = first_error()) != P1HIP_OK) return rc;
     if (coll) {
@@ -777,6 +808,9 @@ int scan_locked(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t upp
         Dev& d = R.devs[i];
         int r = P1HIP_OK;
         const auto g0 = std::chrono::steady_clock::now();
+        // as in phase 1: a host exception (the error strings below allocate)
+        // becomes this device's rc, never std::terminate
+        try {
         if (hipSetDevice(d.ordinal) != hipSuccess) r = fail(P1HIP_ERR_HIP, "hipSetDevice");
         if (!r) {
           ncclResult_t nr = ncclAllGather(d.d_res, d.d_gather, 2, ncclUint64, d.comm, d.stream);
@@ -789,6 +823,9 @@ int scan_locked(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t upp
         d.acc.gather_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g0).count();
         rcs[i] = r;
         if (r) errs[i] = g_err;
+        } catch (...) {
+          rcs[i] = P1HIP_ERR_HIP;  // errs[i] stays empty: building it may be what threw
+        }
       });
       if ((rc = first_error()) != P1HIP_OK) return rc;
     }
@@ -799,7 +836,6 @@ int scan_locked(const uint8_t* msg, size_t msg_len, uint64_t lower, uint64_t upp
       R.stats.fast_launches += d.fast_launches;
       R.stats.fast_nonces += d.fast_nonces;
       R.stats.fast_alg_ops += d.fast_ops;
-      R.stats.fast_kernel_ms += d.fast_ms;
       R.stats.generic_launches += d.gen_launches;
       R.stats.generic_nonces += d.gen_nonces;
       R.stats.scan_launches += d.scan_launches;
@@ -937,7 +973,39 @@ int p1hip_get_device_stats(int index, p1hip_device_stats_t* out) {
 
 const char* p1hip_last_error(void) { return g_err.c_str(); }
 
-const char* p1hip_version(void) { return "p1hip 0.3 gfx950"; }
+const char* p1hip_version(void) { return "p1hip 0.4 gfx950"; }
+
+const char* p1hip_test_knobs(void) {
+  static thread_local std::string s;
+  s.clear();
+  if (!test_knobs_on()) return s.c_str();
+  s = "P1HIP_TEST_KNOBS=1";
+  for (const char* k : kTestKnobs)
+    if (const char* v = test_knob(k)) s += std::string(";") + k + "=" + v;
+  return s.c_str();
+}
+
+int p1hip_device_info(int index, p1hip_device_info_t* out) {
+  if (!out) return fail(P1HIP_ERR_ARGS, "null info pointer");
+  return guarded([&]() {
+    Runtime& R = rt();
+    std::lock_guard<std::mutex> g(R.mu);
+    if (index < 0 || (size_t)index >= R.devs.size()) return fail(P1HIP_ERR_ARGS, "device index out of range");
+    const int o = R.devs[(size_t)index].ordinal;
+    memset(out, 0, sizeof *out);
+    out->ordinal = o;
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, o));
+    HIPCHK(hipDeviceGetPCIBusId(out->pci_bus_id, (int)sizeof out->pci_bus_id - 1, o));
+    out->cu_count = prop.multiProcessorCount;
+    out->clock_khz = prop.clockRate;
+    out->hbm_bytes = (uint64_t)prop.totalGlobalMem;
+    strncpy(out->arch, prop.gcnArchName, sizeof out->arch - 1);
+    static_assert(sizeof(prop.uuid.bytes) == sizeof(out->uuid), "uuid size");
+    memcpy(out->uuid, prop.uuid.bytes, sizeof out->uuid);
+    return P1HIP_OK;
+  });
+}
 
 void p1hip_shutdown(void) {
   Runtime& R = rt();

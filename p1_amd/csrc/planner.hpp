@@ -263,14 +263,22 @@ inline std::string add_fast(const Prefix& P, const Layout& Y, uint64_t hs, uint6
   }
   // units are always in the last word; mode 3 = only the hundreds digit in
   // word FV, mode 4 = tens (and hundreds) in word FV
-  const int mode = var.mode;
+  int mode = var.mode;
   if ((mode == 3 || mode == 4) && dlt[0][0] != 0)
     return "internal: split variant with the units digit in the outer word";
   if (mode == 3 && dlt[1][0] != 0) return "internal: mode 3 with the tens digit in the outer word";
   if (mode == 4 && dlt[1][0] == 0) return "internal: mode 4 without the tens digit in the outer word";
   // the kernel reads the per-nonce word of modes 6 (word FV) and 3/4 (word
-  // FV+1) from lane 0 only: no hi digit may sit in it (last hi byte: qv - k)
-  if ((mode == 6 && qv - k >= 4 * fv) || ((mode == 3 || mode == 4) && qv - k >= 4 * (fv + 1)))
+  // FV+1) from lane 0 only: no hi digit may sit in it (last hi byte: qv - k).
+  // fast_variant only picks mode 6 when that holds; should a later layout
+  // change break it, the scan falls back to mode 1 (the same word per lane,
+  // slower, still exact) rather than failing.  Modes 3/4 have no shipped
+  // per-lane twin (mode 2 is an A/B build), so there it stays an error; the
+  // CPU replay runs every (L+1)%64 x digit count x k through this function
+  // (tests/test_host_logic.py test_emu_every_tail_layout*), so it cannot fire
+  // unnoticed.
+  if (mode == 6 && qv - k >= 4 * fv) mode = 1;
+  if ((mode == 3 || mode == 4) && qv - k >= 4 * (fv + 1))
     return "internal: hi digit in the wave-uniform per-nonce word";
   FastArgs fa;
   memset(&fa, 0, sizeof fa);

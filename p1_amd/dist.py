@@ -5,6 +5,7 @@ xGMI on MI355X; "gloo" in the CPU tests), lexicographic (hash, nonce) min.
 This is the only collective on the path: the reference has
 no exchange step besides the final min of miner.go:56-63.
 """
+import json
 import time
 
 import torch
@@ -81,3 +82,24 @@ def gather_rank_stats(stats, device=None, group=None):
         d.update({k: vf[r * nf + j] for j, k in enumerate(RANK_FLOAT_FIELDS)})
         out.append(d)
     return out
+
+
+IDENTITY_BYTES = 512
+
+
+def gather_rank_identity(ident, device=None, group=None):
+    """All-gather one small JSON-able dict per rank (host name, device
+    ordinal, PCI bus id, UUID ...) as a fixed-size byte record over the same
+    process group, so rank 0 can show which physical GPU each rank ran on.
+    Returns the list of dicts in rank order."""
+    world = dist.get_world_size(group)
+    raw = json.dumps(ident, sort_keys=True).encode()
+    if len(raw) > IDENTITY_BYTES:
+        raise ValueError(f"identity record of {len(raw)} bytes > {IDENTITY_BYTES}")
+    buf = torch.zeros(IDENTITY_BYTES, dtype=torch.uint8)
+    buf[:len(raw)] = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+    t = buf.to(device) if device is not None else buf
+    out = torch.empty(world * IDENTITY_BYTES, dtype=torch.uint8, device=device)
+    dist.all_gather_into_tensor(out, t, group=group)
+    rows = out.cpu().view(world, IDENTITY_BYTES)
+    return [json.loads(bytes(r.tolist()).rstrip(b"\0").decode()) for r in rows]

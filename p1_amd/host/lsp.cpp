@@ -61,13 +61,18 @@ struct Peer {
   bool got_data = false;  // any data message received (heartbeat choice)
   int idle = 0;           // epochs since anything arrived from the peer
   bool lost = false;
+  int copies = 1;         // datagrams per first transmission (Params::Copies)
 };
 
 using SendFn = std::function<void(const Message&)>;
 using DeliverFn = std::function<void(std::string&&)>;
 
+// The first transmission of a message goes out p.copies times (the receiver
+// acks every copy and keeps only new sequence numbers, so a duplicate is
+// harmless); epoch resends go out once, as in the reference.
 void send_data(Peer& p, Peer::Out& o, const SendFn& send) {
-  send(NewData(p.conn_id, o.seq, (int64_t)o.payload.size(), o.payload));
+  const Message m = NewData(p.conn_id, o.seq, (int64_t)o.payload.size(), o.payload);
+  for (int i = o.sent ? 1 : p.copies; i > 0; --i) send(m);
   o.sent = true;
 }
 
@@ -97,15 +102,17 @@ void on_ack(Peer& p, int64_t seq, int window, const SendFn& send) {
 // A data message (Size already checked).  Every copy is acked -- the first
 // ack may have been lost; only new sequence numbers are kept, and delivery
 // is strictly in order (p1.pdf 2.1.2).
-// A correct sender never has a message at or beyond expect + WindowSize in
-// flight (its window starts at its oldest un-acked message, which is at or
-// below our `expect`), so anything that far ahead comes from a faulty peer:
-// it is dropped un-acked, as if lost, which bounds `early` to
-// kEarlyWindows windows instead of letting a peer grow it without limit.
-constexpr int64_t kEarlyWindows = 4;
+// A correct sender never has a message at or beyond expect + ITS WindowSize
+// in flight (its window starts at its oldest un-acked message, which is at or
+// below our `expect`).  The peer's WindowSize is its own Params, not ours
+// (crunner/srunner take -wsize each), so the bound is a fixed generous cap
+// and never our own window: anything kMaxEarly or more ahead is dropped
+// un-acked, as if lost (the sender resends it an epoch later), which bounds
+// `early` instead of letting a faulty peer grow it without limit.
+constexpr int64_t kMaxEarly = 1 << 16;
 void on_data(Peer& p, Message& m, int window, const SendFn& send, const DeliverFn& deliver) {
-  const int64_t ahead = kEarlyWindows * (window > 16 ? window : 16);
-  if (m.SeqNum >= p.expect + ahead) return;
+  (void)window;
+  if (m.SeqNum >= p.expect + kMaxEarly) return;
   send(NewAck(p.conn_id, m.SeqNum));
   p.got_data = true;
   if (m.SeqNum < p.expect) return;
@@ -242,7 +249,8 @@ class ClientImpl : public Client {
   bool Connect(std::string* err) {
     {
       std::lock_guard<std::mutex> g(mu_);
-      send_(NewConnect());
+      p_.copies = prm_.Copies > 1 ? prm_.Copies : 1;
+      for (int i = 0; i < p_.copies; ++i) send_(NewConnect());
     }
     loop_->Start();
     std::unique_lock<std::mutex> lk(mu_);
@@ -448,8 +456,11 @@ class ServerImpl : public Server {
         Conn c;
         c.p.conn_id = id;
         c.p.addr = from;
+        c.p.copies = prm_.Copies > 1 ? prm_.Copies : 1;
         conns_.emplace(id, std::move(c));
         by_addr_[from] = id;
+        // a new connection's Ack goes out `copies` times (first transmission)
+        for (int i = 1; i < conns_[id].p.copies; ++i) conn_->WriteToUDP(Marshal(NewAck(id, 0)), from);
       }
       conn_->WriteToUDP(Marshal(NewAck(id, 0)), from);
       return;

@@ -46,8 +46,22 @@ struct Params {  // params.go:14-26
   int EpochLimit = DefaultEpochLimit;
   int EpochMillis = DefaultEpochMillis;
   int WindowSize = DefaultWindowSize;
+  // Not in the reference: datagrams per FIRST transmission of a Connect, of
+  // a new connection's Ack and of a Data message (epoch resends go out
+  // once).  1 = the reference's behaviour.  Wire-compatible: receivers ack
+  // every copy and deliver each sequence number once, so at a drop rate p a
+  // message is late by a whole epoch only with probability p^Copies instead
+  // of p.  The bitcoin programs use DefaultAppCopies.
+  int Copies = 1;
   std::string String() const;  // params.go:41-44
 };
+
+// Copies used by p1server / p1miner / p1client unless --copies says otherwise.
+// configs[4]'s request crosses ~35 data messages on its critical path (16
+// chunks x Request + Result, Connect, Join ...): at 5% drop, 2 copies still
+// leave ~9% of requests waiting a whole epoch (p^2 per message), 3 copies
+// ~0.4% (tools/bench_lsp.py).
+constexpr int DefaultAppCopies = 3;
 
 Params NewParams();  // params.go:29-35
 

@@ -3,7 +3,7 @@
 // Requests/results are encoding/json bitcoin.Message bytes (miner.go:55,66).
 //
 //   p1miner lsp <host:port> [--device N] [--chunk C] [--epoch-limit K]
-//           [--epoch-millis M] [--window W]
+//           [--epoch-millis M] [--window W] [--copies K]
 //                                        miner.go:13-73: connect, send Join,
 //                                        then Read -> scan -> Write until the
 //                                        connection is lost.  The scan runs on
@@ -48,7 +48,7 @@ static int usage() {
   fprintf(stderr,
           "usage: p1miner scan <msg> <lower> <upper> | hash <msg> <nonce> | "
           "serve [--device N] [--chunk C] | lsp <host:port> [--device N] [--chunk C] [--epoch-limit K] "
-          "[--epoch-millis M] [--window W] | json | lsp-json | lsp-wrap <connID> <seq> | lsp-unwrap\n");
+          "[--epoch-millis M] [--window W] [--copies K] | json | lsp-json | lsp-wrap <connID> <seq> | lsp-unwrap\n");
   return 2;
 }
 
@@ -68,12 +68,14 @@ static int run_lsp(int argc, char** argv) {
   int dev = -1;
   uint64_t chunk = miner::kDefaultChunk;
   lsp::Params prm = lsp::NewParams();
+  prm.Copies = lsp::DefaultAppCopies;
   for (int i = 3; i < argc; ++i) {
     if (!strcmp(argv[i], "--device") && i + 1 < argc) dev = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--chunk") && i + 1 < argc) { if (!parse_u64(argv[++i], &chunk)) return usage(); }
     else if (!strcmp(argv[i], "--epoch-limit") && i + 1 < argc) prm.EpochLimit = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--epoch-millis") && i + 1 < argc) prm.EpochMillis = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--window") && i + 1 < argc) prm.WindowSize = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--copies") && i + 1 < argc) prm.Copies = atoi(argv[++i]);
     else return usage();
   }
   // open the GPU before joining, so the first request does not pay for it

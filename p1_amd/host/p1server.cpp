@@ -240,7 +240,7 @@ class PipeServer {
 
 int usage() {
   fprintf(stderr,
-          "usage: p1server [--chunk C] [--hedge] [--epoch-limit K] [--epoch-millis M] [--window W] [--exit-after N] "
+          "usage: p1server [--chunk C] [--hedge] [--epoch-limit K] [--epoch-millis M] [--window W] [--copies K] [--exit-after N] "
           "lsp <port>\n"
           "       p1server [--chunk C] [--hedge] [--miners N] [--devices d0,d1,..] [--miner-cmd CMD] "
           "scan <msg> <lower> <upper> | serve\n");
@@ -267,6 +267,7 @@ int main(int argc, char** argv) {
   uint64_t chunk = 1ull << 32;
   std::string cmd;
   lsp::Params prm = lsp::NewParams();
+  prm.Copies = lsp::DefaultAppCopies;
   long exit_after = 0;
   int hedge = 1;
   int i = 1;
@@ -286,6 +287,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--epoch-limit") && i + 1 < argc) prm.EpochLimit = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--epoch-millis") && i + 1 < argc) prm.EpochMillis = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--window") && i + 1 < argc) prm.WindowSize = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--copies") && i + 1 < argc) prm.Copies = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--exit-after") && i + 1 < argc) exit_after = atol(argv[++i]);
     else if (!strcmp(argv[i], "--hedge")) hedge = 2;
     else break;

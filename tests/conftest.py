@@ -53,6 +53,9 @@ def gpu():
     # there to exercise the fast kernel variants, so the session turns the
     # small path off (read per scan); tests/test_gpu_small.py turns it back on.
     os.environ["P1HIP_SMALL_MAX_NONCES"] = "0"
+    # the library honours its test knobs only under this master switch
+    # (production ignores them; bench.py refuses to time with it set)
+    os.environ["P1HIP_TEST_KNOBS"] = "1"
     p1_amd.load()
     p1_amd.init_devices([0])
     return p1_amd

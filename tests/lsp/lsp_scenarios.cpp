@@ -2,7 +2,9 @@
 // against this repository's C++ LSP (p1_amd/host/lsp.{hpp,cpp}), one scenario
 // per process run (the fault-injection knobs are process-global).
 //
-//   lsp_scenarios <name>     exit 0 = pass, 1 = fail (reason on stderr)
+//   lsp_scenarios [--copies K] <name>   exit 0 = pass, 1 = fail (reason on
+//                            stderr); --copies sends every first transmission
+//                            K times (lsp::Params::Copies, not in the reference)
 //   lsp_scenarios --list     names
 //
 // Scenarios and parameters follow /root/reference/src/github.com/cmu440/lsp:
@@ -67,11 +69,14 @@ int rnd(int n) {
   return n > 0 ? (int)(r() % (unsigned)n) : 0;
 }
 
+int g_copies = 1;  // --copies K: Params::Copies of every endpoint (1 = the reference)
+
 lsp::Params P(int limit, int ms, int w) {
   lsp::Params p;
   p.EpochLimit = limit;
   p.EpochMillis = ms;
   p.WindowSize = w;
+  p.Copies = g_copies;
   return p;
 }
 
@@ -169,6 +174,82 @@ bool echo_test(int nclients, lsp::Params prm, int nmsgs, int max_sleep, int drop
   server.join();
   cli.clear();
   srv.reset();
+  return true;
+}
+
+// ----------------------------------------------------------------------------
+// Not in the reference: Params::Copies > 1.  Clients stream numbered messages
+// to an echo server; every side must see each message exactly once and in
+// order, and nothing more arrives after several epochs (of resends and
+// heartbeats) -- a duplicate that slipped through would show up as an extra
+// or out-of-order message.
+// ----------------------------------------------------------------------------
+bool dup_test(int copies, int drop) {
+  lsp::Params prm = P(20, 100, 4);
+  prm.Copies = copies;
+  const int nclients = 3, nmsgs = 150;
+  int port = 0;
+  auto srv = start_server(prm, &port);
+  if (!srv) return false;
+  std::vector<std::unique_ptr<lsp::Client>> cli;
+  for (int i = 0; i < nclients; ++i) {
+    cli.push_back(start_client(port, prm));
+    if (!cli.back()) return false;
+  }
+  lspnet::SetWriteDropPercent(drop);
+  Chan<std::pair<int, std::string>> at_server, at_clients;
+  std::thread server([&] {
+    for (;;) {
+      int id;
+      std::string d;
+      if (!srv->Read(&id, &d)) return;
+      at_server.put({id, d});
+      srv->Write(id, d);
+    }
+  });
+  std::vector<std::thread> ths;
+  for (int c = 0; c < nclients; ++c) {
+    ths.emplace_back([&, c] {
+      for (int i = 0; i < nmsgs; ++i) cli[c]->Write(std::to_string(c) + ":" + std::to_string(i));
+      std::string d;
+      while (cli[c]->Read(&d)) at_clients.put({c, d});
+    });
+  }
+  auto check = [&](Chan<std::pair<int, std::string>>& ch, bool by_conn, const char* who) {
+    std::map<int, int> next;  // sender -> next expected index
+    const auto deadline = steady_clock::now() + seconds(20);
+    for (int k = 0; k < nclients * nmsgs; ++k) {
+      std::pair<int, std::string> e;
+      if (!ch.get(&e, deadline)) { fail(std::string(who) + ": timed out"); return false; }
+      const size_t colon = e.second.find(':');
+      const int c = atoi(e.second.substr(0, colon).c_str()), i = atoi(e.second.substr(colon + 1).c_str());
+      const int key = by_conn ? e.first : c;
+      if (!by_conn && c != e.first) { fail(std::string(who) + ": client got another client's echo"); return false; }
+      if (i != next[key]) {
+        fail(std::string(who) + ": message " + e.second + " out of order or duplicated (want index " +
+             std::to_string(next[key]) + ")");
+        return false;
+      }
+      next[key]++;
+    }
+    return true;
+  };
+  bool ok = check(at_server, true, "server") && check(at_clients, false, "clients");
+  if (ok) {
+    // 6 epochs of resends / heartbeats: no message may be delivered again
+    std::pair<int, std::string> e;
+    if (at_server.get(&e, steady_clock::now() + milliseconds(600)) ||
+        at_clients.get(&e, steady_clock::now() + milliseconds(10))) {
+      fail("extra delivery after the stream: " + e.second);
+      ok = false;
+    }
+  }
+  bail_if_failed(ok);
+  lspnet::ResetDropPercent();
+  for (auto& c : cli) c->Close();
+  for (auto& t : ths) t.join();
+  srv->Close();
+  server.join();
   return true;
 }
 
@@ -658,6 +739,10 @@ bool varlen_test(bool server_reads, int timeout_ms) {
 
 const std::map<std::string, std::function<bool()>>& scenarios() {
   static const std::map<std::string, std::function<bool()>> m = {
+      // not in the reference: first transmissions sent 3x (Params::Copies),
+      // every message delivered exactly once, in order, both directions
+      {"DuplicatesExactlyOnce", [] { return dup_test(3, 0); }},
+      {"DuplicatesUnderDrop", [] { return dup_test(2, 15); }},
       // lsp1_test.go
       {"Basic1", [] { return echo_test(1, P(5, 2000, 1), 3, 0, 0, 2000); }},
       {"Basic2", [] { return echo_test(1, P(5, 2000, 1), 50, 0, 0, 2000); }},
@@ -716,8 +801,13 @@ const std::map<std::string, std::function<bool()>>& scenarios() {
 }  // namespace
 
 int main(int argc, char** argv) {
+  if (argc == 4 && std::string(argv[1]) == "--copies") {  // [--copies K] <scenario>
+    g_copies = atoi(argv[2]);
+    argv += 2;
+    argc -= 2;
+  }
   if (argc != 2) {
-    fprintf(stderr, "usage: %s <scenario> | --list\n", argv[0]);
+    fprintf(stderr, "usage: %s [--copies K] <scenario> | --list\n", argv[0]);
     return 2;
   }
   const std::string name = argv[1];

@@ -13,9 +13,12 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def test_single_gpu_defaults_to_c2():
+def test_single_gpu_defaults_to_c4():
+    # north_star's scaling job [0, 2^38) at every N, so
+    # BENCH's N = 1 line and SCALE's 1/2/4/8 points time the same workload
     r = bench.resolve_run(1, None, {}, visible=1)
-    assert r["mode"] == "single" and r["n"] == 1 and r["config"] == "c2"
+    assert r["mode"] == "single" and r["n"] == 1 and r["config"] == "c4"
+    assert [c for c, _, _ in bench.SUB_CONFIGS] == ["c2", "c3"]
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
@@ -109,3 +112,73 @@ def test_scaling_report_names_the_straggler():
     want_frac = (1 << 30) * 1384 / 0.1 / bench.VALU_PEAK_OPS
     assert abs(rep["units"][0]["frac"] - want_frac) < 1e-12
     assert rep["gather_ms_per_step_max"] == 0.05
+
+
+def _stats(nonces, kernel_ms, b_tail=1, launches=1):
+    return {"scan_kernel_ms": kernel_ms, "scan_launches": launches, "scan_nonces": nonces,
+            "scan_alg_ops": nonces * 1384 * b_tail, "fast_nonces": nonces, "generic_nonces": 0}
+
+
+def test_roofline_assembly_c4_fractions_below_one():
+    """A realistic c4 run (2^38 nonces in 7.43 s) assembles with every frac
+    field <= 1, the one 78.64 T peak, no survey-peak fraction, and the mix
+    comparison named as a speed ratio."""
+    cfg = bench.CONFIGS["c4"]
+    pmc = {"valu_wave_instr_per_nonce": 1186.3, "effective_clock_GHz": 2.384, "hbm_bytes_per_launch": 1.6e6}
+    roof = bench.assemble_roofline("c4", cfg, _stats(1 << 38, 7430.0), 1, pmc, "x", (7.427e9, "y"))
+    assert abs(roof["peak"] - 78.6432) < 1e-9
+    assert 0.6 < roof["frac"] < 0.7 and 0.6 < roof["frac_rocprof"] < 0.7
+    assert 0.5 < roof["executed"]["frac"] < 0.6
+    assert "frac_vs_survey_peak" not in roof
+    mix = roof.get("unhoisted_mix")
+    if mix:
+        assert "frac" not in mix and mix["speed_vs_unhoisted_mix"] > 1.0
+
+
+def test_roofline_assembly_rejects_frac_above_one():
+    # the same 2^38 nonces "in" 2 s would be 1.9x the peak: refused, not printed
+    cfg = bench.CONFIGS["c4"]
+    with pytest.raises(bench.RooflineError):
+        bench.assemble_roofline("c4", cfg, _stats(1 << 38, 2000.0), 1)
+    with pytest.raises(bench.RooflineError):
+        bench.assemble_roofline("c2", bench.CONFIGS["c2"], _stats(1 << 32, 117.0), 1, rocprof=(30e6, "z"))
+    with pytest.raises(bench.RooflineError):
+        bench.check_fracs({"a": {"frac_x": 1.01}}, 1)
+    bench.check_fracs({"a": {"frac_x": 1.01}}, 2)  # 2-block: the algorithmic count is not a utilisation
+
+
+def test_roofline_two_block_config_names_the_algorithmic_ratio():
+    cfg = bench.CONFIGS["c3"]
+    pmc = {"valu_wave_instr_per_nonce": 893.6, "effective_clock_GHz": 2.375}
+    roof = bench.assemble_roofline("c3", cfg, _stats(1 << 34, 343.0, b_tail=2), 1, pmc, "x")
+    assert roof["alg_ops_over_peak"] > 1.0  # hoisting + MODE 5: not a utilisation
+    assert roof["frac"] is not None and roof["frac"] < 1.0
+
+
+def test_rocprof_row_reads_committed_summary():
+    avg, src = bench.rocprof_row("c2")
+    assert avg and 100e6 < avg < 130e6 and src.startswith("profiles/")
+
+
+def test_bench_refuses_test_knobs():
+    """with the master switch set, bench.py exits 4
+    before touching a device (no GPU here)."""
+    env = dict(os.environ, P1HIP_TEST_KNOBS="1", P1HIP_NO_TABLE="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert p.returncode == 4, (p.returncode, p.stderr[-2000:])
+    assert "P1HIP_NO_TABLE" in p.stderr and "test knobs" in p.stderr
+
+
+def test_library_ignores_knobs_without_master_switch(monkeypatch):
+    import p1_amd
+
+    monkeypatch.setenv("P1HIP_TEST_FAIL_DEVICE", "0")
+    monkeypatch.setenv("P1HIP_TEST_KNOBS", "0")
+    assert p1_amd.test_knobs() == {}
+    monkeypatch.setenv("P1HIP_TEST_KNOBS", "1")
+    assert p1_amd.test_knobs() == {"P1HIP_TEST_KNOBS": "1", "P1HIP_TEST_FAIL_DEVICE": "0"}
+    monkeypatch.delenv("P1HIP_TEST_KNOBS")
+    assert p1_amd.test_knobs() == {}

@@ -77,7 +77,7 @@ def _stats_worker(rank, world, port, q):
     import torch.distributed as dist
 
     import oracle
-    from p1_amd.dist import distributed_scan, gather_rank_stats
+    from p1_amd.dist import distributed_scan, gather_rank_identity, gather_rank_stats
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -90,8 +90,10 @@ def _stats_worker(rank, world, port, q):
             "scan_ms": timing["scan_s"] * 1e3, "gather_ms": timing["gather_s"] * 1e3, "elapsed_ms": 10.0 + rank,
             "step_ms_median": 3.25}
     got = gather_rank_stats(mine)
+    ident = gather_rank_identity({"hostname": "host-" + "é" * rank, "ordinal": rank, "pci_bus_id": f"0000:{rank:02x}:00.0",
+                                  "uuid": f"{rank:032x}", "rank": rank})
     dist.destroy_process_group()
-    q.put((rank, timing["steps"], timing["shard"], got))
+    q.put((rank, timing["steps"], timing["shard"], got, ident))
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -110,7 +112,11 @@ def test_gather_rank_stats_gloo(world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, steps, shard, got in res:
+    for rank, steps, shard, got, ident in res:
+        # bench.py's per-rank device identity: one record per rank, in rank order
+        assert [i["rank"] for i in ident] == list(range(world))
+        assert [i["pci_bus_id"] for i in ident] == [f"0000:{r:02x}:00.0" for r in range(world)]
+        assert ident[world - 1]["hostname"] == "host-" + "é" * (world - 1)
         assert steps == 3 and tuple(shard) == shard_range(0, 9999, rank, world)
         assert len(got) == world
         for r, g in enumerate(got):

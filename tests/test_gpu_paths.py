@@ -41,6 +41,7 @@ def reinit(gpu, monkeypatch):
     for k in ("P1HIP_MIN_FAST_THREADS", "P1HIP_FORCE_RCCL", "P1HIP_TEST_FAIL_DEVICE", "P1HIP_NO_RCCL",
               "P1HIP_NO_TABLE"):
         monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("P1HIP_TEST_KNOBS", "1")
     gpu.shutdown()
     gpu.init_devices([0])
 
@@ -304,6 +305,29 @@ def test_failure_on_one_device_does_not_hang(reinit, oracle_mod):
     # the library is usable afterwards
     g = reinit((0,), P1HIP_TEST_FAIL_DEVICE=-1, P1HIP_FORCE_RCCL=0)
     assert g.scan("bradfitz", 0, 9999) == (1419516646206828, 9898)
+
+
+def test_test_knobs_are_fenced_off_production(reinit):
+    """a stray test knob in a production environment
+    changes nothing.  P1HIP_TEST_FAIL_DEVICE=0 without the master switch
+    P1HIP_TEST_KNOBS=1 is ignored (the scan succeeds and p1hip_test_knobs()
+    reports nothing); with the switch it is honoured (rc -2) and reported."""
+    g = reinit(P1HIP_TEST_KNOBS=0, P1HIP_TEST_FAIL_DEVICE=0, P1HIP_NO_TABLE=1)
+    assert g.test_knobs() == {}
+    assert g.scan("bradfitz", 0, 99999) == (85364550342847, 98985)  # = oracle
+    g = reinit(P1HIP_TEST_KNOBS=1, P1HIP_TEST_FAIL_DEVICE=0)
+    assert g.test_knobs()["P1HIP_TEST_FAIL_DEVICE"] == "0"
+    with pytest.raises(g.P1HipError) as e:
+        g.scan("bradfitz", 0, 99999)
+    assert e.value.rc == -2 and "injected" in str(e.value)
+    g = reinit(P1HIP_TEST_FAIL_DEVICE=-1)
+
+
+def test_device_info_names_the_gpu(gpu):
+    info = gpu.device_info(0)
+    assert info["ordinal"] == 0 and info["arch"].startswith("gfx950")
+    assert info["cu_count"] == 256 and info["hbm_bytes"] > 200 << 30
+    assert len(info["pci_bus_id"].split(":")) == 3, info
 
 
 def test_config5_full_size_split_over_8_miner_processes(gpu, oracle_mod, large):

@@ -26,6 +26,9 @@ SCENARIOS = [f"Basic{i}" for i in range(1, 10)] + [f"SendReceive{i}" for i in ra
      "ServerCloseConns2", "ClientClose1", "ClientClose2"] + \
     [f"{m}{i}" for m in ("ServerFastClose", "ServerToClient", "ClientToServer", "RoundTrip") for i in range(1, 4)] + \
     ["VariableLengthMsgServer", "VariableLengthMsgClient"]
+# not in the reference: Params::Copies > 1 (first transmissions sent k times)
+# delivers every message exactly once, in order, with and without loss
+DUPLICATE_SCENARIOS = ["DuplicatesExactlyOnce", "DuplicatesUnderDrop"]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -36,11 +39,17 @@ def built():
 
 def test_driver_lists_every_scenario():
     out = subprocess.run([DRIVER, "--list"], capture_output=True, text=True, check=True).stdout.split()
-    assert sorted(out) == sorted(SCENARIOS)
+    assert sorted(out) == sorted(SCENARIOS + DUPLICATE_SCENARIOS)
 
 
-@pytest.mark.parametrize("name", SCENARIOS)
-def test_reference_scenario(name):
-    r = subprocess.run([DRIVER, name], capture_output=True, text=True, timeout=120)
+@pytest.mark.parametrize("copies", [1, 2])
+@pytest.mark.parametrize("name", SCENARIOS + DUPLICATE_SCENARIOS)
+def test_reference_scenario(name, copies):
+    """copies 1: the reference's protocol; copies 2: what the bitcoin
+    programs run by default (lsp::DefaultAppCopies) -- the reference's
+    scenarios must pass unchanged with every first transmission doubled."""
+    if name in DUPLICATE_SCENARIOS and copies == 2:
+        pytest.skip("sets its own Copies")
+    r = subprocess.run([DRIVER, "--copies", str(copies), name], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith(f"{name} PASS")

@@ -263,9 +263,11 @@ def _udp_frames(sock, seconds):
 
 
 def test_far_ahead_data_is_dropped_unacked(system):
-    """a peer's data far beyond the window (SeqNum >= expect +
-    4 x max(window, 16)) is dropped without an ack instead of being buffered
-    without bound; in-window data is acked and delivered in order."""
+    """a peer's data far ahead of the receiver (SeqNum >=
+    expect + 2^16) is dropped without an ack instead of being buffered
+    without bound; data ahead by more than the RECEIVER's own window (a peer
+    with a larger WindowSize, its own Params) is buffered, acked and
+    delivered in order."""
     import base64
     import json as _json
     import socket as _socket
@@ -283,13 +285,14 @@ def test_far_ahead_data_is_dropped_unacked(system):
         return _json.dumps({"Type": 1, "ConnID": cid, "SeqNum": seq, "Size": len(join),
                             "Payload": base64.b64encode(join).decode()}).encode()
 
-    sock.send(data(1 + 64))  # expect is 1: 64 ahead = the bound for window 1
+    sock.send(data(1 + (1 << 16)))  # expect is 1: 2^16 ahead = the bound
     acks = [f["SeqNum"] for f in _udp_frames(sock, 0.5) if f["Type"] == 2]
-    assert 65 not in acks
+    assert 1 + (1 << 16) not in acks
     sock.send(data(2))  # one ahead: buffered and acked
+    sock.send(data(100))  # 99 ahead of a window-1 server: a larger peer window, buffered and acked
     sock.send(data(1))
     acks = [f["SeqNum"] for f in _udp_frames(sock, 0.5) if f["Type"] == 2]
-    assert 2 in acks and 1 in acks
+    assert 2 in acks and 1 in acks and 100 in acks
     sock.close()
 
 

@@ -28,8 +28,8 @@ def _cpu_flags():
         return ""
 
 
-pytestmark = pytest.mark.skipif(not (" sha_ni" in _cpu_flags() and " avx512f" in _cpu_flags()),
-                                reason="pin_large needs the x86 SHA extensions and AVX-512 (container CPU)")
+needs_sha = pytest.mark.skipif(not (" sha_ni" in _cpu_flags() and " avx512f" in _cpu_flags()),
+                               reason="pin_large needs the x86 SHA extensions and AVX-512 (container CPU)")
 
 
 def go_hash(m, n):
@@ -37,6 +37,9 @@ def go_hash(m, n):
 
 
 def test_validation_record_matches_tool_source(golden):
+    """Runs on every CPU (no SHA extensions needed): an edited pin_large.c
+    cannot leave stale pins behind, and every pin is labelled as not covered
+    by a reference-held fixture."""
     rec = json.load(open(pin.VALID))
     assert rec["tool_sha16"] == pin.src_sha(), "pin_large.c changed since it was validated: re-run validate"
     assert all(c["ok"] for c in rec["checks"])
@@ -45,9 +48,12 @@ def test_validation_record_matches_tool_source(golden):
     # every large golden answer came from this validated tool (or the survey's hashlib run)
     for v in golden["scan"]:
         if v.get("large") and "pin_large" in v["source"]:
-            assert v["tool_sha16"] == rec["tool_sha16"]
+            assert v["tool_sha16"] == rec["tool_sha16"] == pin.src_sha()
+        if v.get("large"):
+            assert v["reference_pinned"] is False and v["parity"].startswith("parity-unpinned")
 
 
+@needs_sha
 @pytest.mark.parametrize("sha_only", [False, True], ids=["avx512+sha", "sha-ni"])
 def test_golden_scans(golden, sha_only):
     for v in golden["scan"]:
@@ -58,6 +64,7 @@ def test_golden_scans(golden, sha_only):
         assert (r["hash"], r["nonce"]) == (v["hash"], v["nonce"]), v
 
 
+@needs_sha
 def test_random_hashes_vs_hashlib():
     rnd = random.Random(7)
     for _ in range(200):
@@ -72,6 +79,7 @@ def test_random_hashes_vs_hashlib():
     (b"bradfitz", 10**10 - 10**7, 10**10 + 10**7 - 1),          # decade straddle on both paths
     (M120, (1 << 34) - 5 * 10**6, (1 << 34) - 1),              # two tail blocks, cached first block
 ], ids=["c4-top", "bradfitz-straddle", "c3-top"])
+@needs_sha
 def test_subranges_vs_oracle(oracle_mod, m, lo, hi):
     want = oracle_mod.scan(m, lo, hi, threads=8)
     for sha_only in (False, True):
@@ -79,6 +87,7 @@ def test_subranges_vs_oracle(oracle_mod, m, lo, hi):
         assert (r["hash"], r["nonce"]) == want, sha_only
 
 
+@needs_sha
 def test_chunk_results_resume_from_checkpoint(tmp_path, oracle_mod):
     ck = str(tmp_path / "ck")
     lo, hi = 10**9, 10**9 + 3 * 10**6

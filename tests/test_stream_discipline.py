@@ -19,7 +19,7 @@ SRC = os.path.join(ROOT, "p1_amd", "csrc", "p1hip.hip")
 
 # host-side management calls that enqueue nothing on any stream
 STREAM_FREE = {
-    "hipEventCreate", "hipEventDestroy", "hipEventElapsedTime", "hipEventSynchronize", "hipFree",
+    "hipDeviceGetPCIBusId", "hipEventCreate", "hipEventDestroy", "hipEventElapsedTime", "hipEventSynchronize", "hipFree",
     "hipGetDeviceCount", "hipGetDeviceProperties", "hipGetErrorString", "hipGetLastError", "hipHostFree",
     "hipHostMalloc", "hipMalloc", "hipModuleGetFunction", "hipModuleLoadData", "hipModuleUnload",
     "hipSetDevice", "hipStreamCreateWithFlags", "hipStreamDestroy", "hipStreamSynchronize",

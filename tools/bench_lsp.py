@@ -11,7 +11,9 @@ env: MINERS (8), NGPU (1), UPPER (2^36 - 1), CHUNK (2^32), WINDOW (8),
      DROP (5), REPS (3), EPOCH_MS (unset: the reference's 2000 ms epochs;
      a lost datagram is resent one epoch later, so at 5% drop the wall time
      holds whole epochs), HEDGE=1 (p1server --hedge: idle miners run copies
-     of the chunks in flight longest); FAKE=1 runs the CPU oracle-backed miner double
+     of the chunks in flight longest), COPIES (unset: the programs' default,
+     lsp::DefaultAppCopies = 3; 1 = the reference protocol: datagrams per
+     first transmission); FAKE=1 runs the CPU oracle-backed miner double
      (tools/lsp_fake_miner, test plumbing only) instead of p1miner
 Reference: server.go:45-170 (dispatch), miner.go:13-73, client.go:21."""
 import json
@@ -49,6 +51,9 @@ def main():
     epoch = os.environ.get("EPOCH_MS")
     if epoch:
         lsp += ["--epoch-millis", epoch]
+    copies = os.environ.get("COPIES")
+    if copies:
+        lsp += ["--copies", copies]
     procs = []
     try:
         hedge = os.environ.get("HEDGE") == "1"
@@ -63,6 +68,11 @@ def main():
         for i in range(miners):
             argv = [FAKE, hp] + lsp if fake else [MINER, "lsp", hp, "--device", str(i % ngpu)] + lsp
             procs.append(subprocess.Popen(argv, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env))
+
+        time.sleep(0.5)
+        dead = [p.args for p in procs[1:] if p.poll() is not None]
+        if dead:
+            raise SystemExit(f"bench_lsp: miner exited at start: {dead[0]}")
 
         def request():
             t0 = time.perf_counter()
@@ -86,7 +96,9 @@ def main():
             "workload": f"configs[4]: client 'bradfitz' maxNonce {upper} -> p1server lsp (chunks of {chunk}) -> "
                         f"{miners} {'CPU oracle miner doubles' if fake else f'p1miner lsp processes on {ngpu} GPU(s)'}"
                         f"; LSP window {window}, {drop}% write drop in every process, "
-                        f"{epoch or 'default (2000)'} ms epochs{', tail hedging' if hedge else ''}",
+                        f"{epoch or 'default (2000)'} ms epochs{', tail hedging' if hedge else ''}, "
+                        f"{copies or 'default (3)'} copies per first transmission",
+            "copies": int(copies) if copies else 3, "epoch_ms": int(epoch) if epoch else 2000, "miners": miners,
             "reps": reps, "wall_s": walls, "wall_s_median": med, "warmup_wall_s": warm_s,
             "GH_s": (upper + 1) / med / 1e9,
             "result": results[-1], "consistent": all(r == results[0] for r in results),

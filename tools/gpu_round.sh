@@ -24,7 +24,7 @@ step() {  # step <name> <timeout> <cmd...>
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 600 python "$ROOT/bench.py" ${BENCH_ARGS:-} > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
 [ -z "${EXTRA_BENCH:-}" ] || step bench_extra 600 python "$ROOT/bench.py" $EXTRA_BENCH > "$OUT/${TAG}_bench_extra.json" 2> "$OUT/${TAG}_bench_extra.err"
 for cfg in ${BENCH_CONFIGS:-}; do
-  step bench_$cfg 600 python "$ROOT/bench.py" --config $cfg --steps ${CFG_STEPS:-3} --warmup 1 --no-cpu > "$OUT/${TAG}_bench_$cfg.json" 2> "$OUT/${TAG}_bench_$cfg.err"
+  step bench_$cfg 600 python "$ROOT/bench.py" --config $cfg --steps ${CFG_STEPS:-3} --warmup 1 --no-cpu --no-by-config > "$OUT/${TAG}_bench_$cfg.json" 2> "$OUT/${TAG}_bench_$cfg.err"
 done
 [ "${RUN_SWEEP:-0}" != 1 ] || step sweep 900 python "$ROOT/tools/sweep.py" > "$OUT/${TAG}_sweep.jsonl" 2> "$OUT/${TAG}_sweep.err"
 [ "${RUN_SERVER:-0}" != 1 ] || step bench_server 900 python "$ROOT/tools/bench_server.py" > "$OUT/${TAG}_bench_server.json" 2> "$OUT/${TAG}_bench_server.err"
@@ -39,18 +39,18 @@ if [ "${RUN_DIST1:-0}" = 1 ]; then
 fi
 for lib in ${VARIANTS:-}; do
   n=$(basename "$lib" .so)
-  P1HIP_LIB="$ROOT/$lib" step "bench_$n" 600 python "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu > "$OUT/${TAG}_bench_$n.json" 2> "$OUT/${TAG}_bench_$n.err"
+  P1HIP_LIB="$ROOT/$lib" step "bench_$n" 600 python "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu --no-by-config > "$OUT/${TAG}_bench_$n.json" 2> "$OUT/${TAG}_bench_$n.err"
 done
 cd /tmp && export TMPDIR=/tmp
 # kernel-trace stats and PMC passes per config (every k_scan launch of the
 # profiled command is a workload launch: --no-small-request)
 for cfg in ${PROF_CONFIGS:-c2}; do
-  pargs="--steps 1 --warmup 0 --no-cpu --no-small-request --config $cfg"
+  pargs="--steps 1 --warmup 0 --no-cpu --no-small-request --no-by-config --config $cfg"
   if [ "${SKIP_PROF:-0}" != 1 ]; then
     # the kernel trace of a bench run shaped like the timed one (warm-up
     # steps, then timed steps): summarize_prof --skip-launches 2 averages the
     # same launches bench.py's HIP events time
-    step rocprof_stats_$cfg 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_${cfg}_prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps ${PROF_STEPS:-3} --warmup 2 --no-cpu --no-small-request --config $cfg > "$OUT/${TAG}_${cfg}_prof_bench.json"
+    step rocprof_stats_$cfg 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_${cfg}_prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps ${PROF_STEPS:-3} --warmup 2 --no-cpu --no-small-request --no-by-config --config $cfg > "$OUT/${TAG}_${cfg}_prof_bench.json"
   fi
   if [ "${SKIP_PMC:-0}" != 1 ]; then
     i=0

@@ -138,7 +138,11 @@ def pin(name):
     entry = {"msg_hex": m.hex(), "lower": lo, "upper": hi, "hash": r["hash"], "nonce": r["nonce"],
              "source": "tools/pin_large.c (container-only SHA-NI/AVX-512 restatement, validated: "
                        "tests/golden/pin_large_validation.json)",
-             "large": True, "config": desc,
+             "large": True, "config": desc, "reference_pinned": False,
+             "parity": ("parity-unpinned: no reference-held fixture covers this range (the reference's own "
+                        "vectors are the p1.pdf known answers and the 4 mtest outputs, Upper <= 9999999); the "
+                        "answer comes from an independent CPU restatement of the same algorithm, validated "
+                        "against the oracle on smaller ranges"),
              "command": "python tools/pin_large.py pin " + name + "  ->  " + " ".join(
                  ["tools/pin_large"] + cmd[1:6]),
              "tool_sha16": src_sha(), "wall_s_last_invocation": round(wall, 1),
