@@ -481,22 +481,41 @@ def device_identity(index):
             "uuid": info["uuid"], "arch": info["arch"], "cu_count": info["cu_count"]}
 
 
-def timed_steps(step, steps, warmup, barrier):
+class Progress:
+    """A line on stderr at most every `every` seconds (rank 0 only): a c4
+    run at N = 1 takes minutes before its one stdout line, and a silent
+    process looks hung to a watchdog.  stdout stays the single JSON line."""
+
+    def __init__(self, label, on=True, every=15.0):
+        self.label, self.on, self.every = label, on, every
+        self.last = time.perf_counter()
+
+    def __call__(self, what, i, n):
+        now = time.perf_counter()
+        if self.on and (now - self.last >= self.every or i == n):
+            print(f"bench.py: {self.label} {what} {i}/{n}", file=sys.stderr, flush=True)
+            self.last = now
+
+
+def timed_steps(step, steps, warmup, barrier, progress=None):
     """W untimed steps, then K timed ones bracketed by barrier() (a
     torch.distributed barrier + device synchronise); library stats reset and
     HIP-event profiling on over exactly the timed steps."""
     import p1_amd
 
-    for _ in range(warmup):
+    progress = progress or (lambda *a: None)
+    for i in range(warmup):
         step()
+        progress("warm-up step", i + 1, warmup)
     p1_amd.reset_stats()
     p1_amd.set_profiling(True)
     barrier()
     t0 = time.perf_counter()
     results, marks = [], [t0]
-    for _ in range(steps):
+    for i in range(steps):
         results.append(step())  # synchronous: the (hash, nonce) result is on the host
         marks.append(time.perf_counter())
+        progress("timed step", i + 1, steps)  # a few µs between steps, after the mark
     barrier()
     elapsed = time.perf_counter() - t0
     p1_amd.set_profiling(False)
@@ -517,7 +536,7 @@ def sub_result(name, warmup, steps, sync):
     cfg = CONFIGS[name]
     total = job_total(cfg, 1)
     elapsed, step_ms, results, stats = timed_steps(lambda: p1_amd.scan(cfg["msg"], 0, total - 1), steps, warmup,
-                                                   sync)
+                                                   sync, Progress(name))
     pmc, pmc_src = pmc_summary(name)
     roof = assemble_roofline(name, cfg, stats, steps, pmc, pmc_src, rocprof_row(name))
     known, src = known_answer(cfg, 1)
@@ -619,10 +638,12 @@ def main():
         for d in sync_devs:
             torch.cuda.synchronize(d)
 
-    for _ in range(args.warmup):
+    progress = Progress(run["config"], on=(rank == 0))
+    for i in range(args.warmup):
         step()
+        progress("warm-up step", i + 1, args.warmup)
     timing.clear()
-    elapsed, step_ms, results, stats = timed_steps(step, args.steps, 0, barrier)
+    elapsed, step_ms, results, stats = timed_steps(step, args.steps, 0, barrier, progress)
 
     if mode == "torchrun":
         from p1_amd.dist import gather_rank_identity, gather_rank_stats
@@ -738,6 +759,7 @@ def main():
                                      "matches_known": tuple(small) == (1419516646206828, 9898),
                                      "median_latency_us": lat[len(lat) // 2] * 1e6}
         if n_gpus == 1 and not args.no_cpu:
+            print("bench.py: cpu_baseline", file=sys.stderr, flush=True)
             line["cpu_baseline"] = cpu_baseline(msg, 1 << 31, args.cpu_seconds)
         print(json.dumps(line), flush=True)
         wrong = [k for k, v in line.get("by_config", {}).items() if v.get("matches_known") is False]

@@ -37,6 +37,13 @@ if [ "${RUN_DIST1:-0}" = 1 ]; then
   # all-gather of the 16-B partials, all-reduce of the step time) at world 1
   step dist1_nccl 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29512 "$ROOT/bench.py" --gpus 1 --dist --config c4 --steps 2 --warmup 1 --no-cpu > "$OUT/${TAG}_dist1_nccl.json" 2> "$OUT/${TAG}_dist1_nccl.err"
 fi
+# configs[4] end to end over LSP (tools/bench_lsp.py), one run per spec
+# "name:VAR=v,VAR=v" (MINERS, COPIES, EPOCH_MS, REPS, HEDGE ...)
+for spec in ${LSP_RUNS:-}; do
+  name=${spec%%:*}
+  vars=${spec#*:}
+  step "lsp_$name" 600 env ${vars//,/ } python "$ROOT/tools/bench_lsp.py" > "$OUT/${TAG}_lsp_$name.json" 2> "$OUT/${TAG}_lsp_$name.err"
+done
 for lib in ${VARIANTS:-}; do
   n=$(basename "$lib" .so)
   P1HIP_LIB="$ROOT/$lib" step "bench_$n" 600 python "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu --no-by-config > "$OUT/${TAG}_bench_$n.json" 2> "$OUT/${TAG}_bench_$n.err"

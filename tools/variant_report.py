@@ -16,6 +16,7 @@ the shipped pipeline (hipcc -S -> tools/isa_post.py -> code object) and read
     B 2.66 SIMD cycles per wave instruction at 4 waves/SIMD) at 2.35 GHz.
 
 usage: variant_report.py [--jobs N] [--only FV,NV,TR ...] [--waves W] > out.jsonl
+       variant_report.py --explain [report.jsonl ...]   (FV-floor decomposition)
 """
 import argparse
 import concurrent.futures as cf
@@ -140,13 +141,55 @@ def build_one(v, waves, isapost):
         return r
 
 
+def explain(paths, ref=(4, 6, False)):
+    """per-nonce loop VALU of every 1-block (non-TRAIL)
+    digit-update variant against `ref` (c2's 4,6), split into what the lost
+    hoisting explains -- each FV step below ref moves one round and one
+    schedule word into the loop (the ref family's own per-FV step, read off
+    FV, FV+1 of the same mode) and mode 1 vs 6 the wave-uniform word -- and
+    the rest, which would be an attributable target."""
+    rows = {}
+    for p in paths:
+        for ln in open(p):
+            if ln.startswith("{"):
+                d = json.loads(ln)
+                rows[tuple(d["variant"])] = d["loop"]
+    base = rows[ref]
+    # the per-FV step of the ref mode, measured between neighbouring FVs
+    steps = {fv: rows[(fv, ref[1], False)]["valu"] - rows[(fv + 1, ref[1], False)]["valu"]
+             for fv in range(0, 13) if (fv, ref[1], False) in rows and (fv + 1, ref[1], False) in rows}
+    uniform = rows[(ref[0], 1, False)]["valu"] - base["valu"]  # mode 1 vs 6 at the ref FV
+    out = []
+    for (fv, mode, tr), lp in sorted(rows.items()):
+        if tr or mode not in (1, 3, 4, 6) or fv > ref[0] + 2:
+            continue
+        # split modes 3/4 run the <FV+1, 1> loop per nonce (outer word hoisted)
+        efv = fv + 1 if mode in (3, 4) else fv
+        lost = sum(steps.get(f, 0) for f in range(efv, ref[0])) - sum(steps.get(f, 0) for f in range(ref[0], efv))
+        mode_cost = uniform if mode == 1 else 0  # modes 3/4 keep their inner word uniform too
+        d = lp["valu"] - base["valu"]
+        out.append({"variant": [fv, mode, tr], "loop_valu": lp["valu"], "A": lp["half_rate_A"],
+                    "B": lp["full_rate_B"], "vs_ref": d, "explained_by_fv": lost,
+                    "explained_by_uniform_word": mode_cost, "unexplained": d - lost - mode_cost})
+    return {"ref": list(ref), "ref_valu": base["valu"], "per_fv_step_valu": steps,
+            "mode1_minus_mode6_valu": uniform}, out
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--explain", nargs="*", default=None,
+                    help="read variant report jsonl files and print the FV-floor decomposition instead of building")
     ap.add_argument("--jobs", type=int, default=8)
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--isapost", default="--align-loops=3 --loop-offset=4 --loop-parity")
     a = ap.parse_args()
+    if a.explain is not None:
+        head, rows = explain(a.explain or [os.path.join(ROOT, "profiles/r03f_variant_report.jsonl")])
+        print(json.dumps(head))
+        for r in rows:
+            print(json.dumps(r))
+        return
     vs = variants()
     if a.only:
         want = {tuple(int(x) if x.isdigit() else x == "true" for x in o.split(",")) for o in a.only}
