@@ -574,6 +574,12 @@ def main():
                          "several ranks on one GPU")
     args = ap.parse_args()
 
+    # torch first: its wheel carries its own HIP runtime, and libp1hip.so must
+    # bind to that already-loaded copy.  Loaded the other way round, the
+    # process holds two HIP runtimes and whichever initialises second sees no
+    # device (r04a: "No HIP GPUs are available" / p1hip rc -1).
+    import torch
+
     import p1_amd
     from p1_amd.build import ensure_built
 
@@ -584,8 +590,6 @@ def main():
         print(f"bench.py: refusing to time with library test knobs in force: {knobs} "
               f"(unset P1HIP_TEST_KNOBS)", file=sys.stderr)
         sys.exit(4)
-
-    import torch
 
     visible = torch.cuda.device_count()
     try:

@@ -2,6 +2,11 @@
 
 Fails loudly: a missing library, a missing symbol or a non-zero return code
 raises P1HipError.  Nothing here computes a hash on the CPU.
+
+A process that also uses torch on the GPU must import torch BEFORE the
+library is loaded: the torch wheel ships its own HIP runtime, and
+libp1hip.so has to bind to that copy; the other order leaves two HIP
+runtimes in the process and the second to initialise sees no device.
 """
 import ctypes
 import os

@@ -182,3 +182,13 @@ def test_library_ignores_knobs_without_master_switch(monkeypatch):
     assert p1_amd.test_knobs() == {"P1HIP_TEST_KNOBS": "1", "P1HIP_TEST_FAIL_DEVICE": "0"}
     monkeypatch.delenv("P1HIP_TEST_KNOBS")
     assert p1_amd.test_knobs() == {}
+
+
+def test_bench_imports_torch_before_the_library():
+    """r04a: loading libp1hip.so before torch leaves two HIP runtimes in the
+    process (torch's wheel carries its own) and the second to initialise sees
+    no GPU.  main() must import torch before p1_amd."""
+    import inspect
+
+    src = inspect.getsource(bench.main)
+    assert src.index("import torch\n") < src.index("import p1_amd\n")
