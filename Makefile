@@ -21,7 +21,7 @@ ISAPOST ?= --align-loops=3 --loop-offset=4 --loop-parity
 BUILD := build
 
 all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios \
-     tools/lsp_fake_miner tools/queue_ctl
+     tools/lsp_fake_miner tools/queue_ctl tools/wcal
 
 $(BUILD)/p1hip_kernels.s: $(CSRC)/p1hip_kernels.hip $(DEVHDRS) Makefile
 	mkdir -p $(BUILD)
@@ -76,6 +76,10 @@ tools/lsp_fake_miner: tests/lsp/lsp_fake_miner.cpp p1_amd/host/bitcoin.cpp $(HOS
 tools/queue_ctl: tools/queue_ctl.cpp include/p1hip.h p1_amd/libp1hip.so
 	$(HIPCC) -O2 -std=c++17 -o $@ tools/queue_ctl.cpp -Lp1_amd -lp1hip -Wl,-rpath,'$$ORIGIN/../p1_amd'
 
+# measurement program: WRITE_SIZE/FETCH_SIZE calibration for k_scan's partials
+tools/wcal: tools/wcal.hip
+	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -o $@ tools/wcal.hip
+
 # host-only replay of the kernels' per-thread code (layout tests; not product)
 tools/p1emu: tools/p1emu.cpp $(HDRS)
 	$(HIPCC) -O2 -std=c++17 -DP1_NV2_PLAIN -o $@ tools/p1emu.cpp
@@ -97,7 +101,7 @@ isa: $(BUILD)/p1hip_kernels.post.s
 	$(HIPCC) $(DEVFLAGS) -c -o /dev/null $(CSRC)/p1hip_kernels.hip -Rpass-analysis=kernel-resource-usage 2> $(BUILD)/resource.txt || true
 
 clean:
-	rm -f p1_amd/libp1hip.so tools/queue_ctl tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios tools/lsp_fake_miner
+	rm -f p1_amd/libp1hip.so tools/queue_ctl tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios tools/lsp_fake_miner tools/wcal
 	rm -rf $(BUILD)/p1hip_kernels* $(BUILD)/p1hip_host.o
 	$(MAKE) -C oracle clean
 .PHONY: all oracle clean isa variant

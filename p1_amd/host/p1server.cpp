@@ -18,8 +18,6 @@
 //       Results on stdout, in request order, over child-process miners
 //
 // opts: --chunk C (nonces per miner job, default 2^32)
-//        --hedge: once every chunk is out, idle miners run copies of the chunks
-//          in flight longest, first answer wins (scheduler.hpp); off by default
 //   lsp:   --epoch-limit K --epoch-millis M --window W (lsp.Params; default
 //          NewParams(): 5, 2000, 1).  P1LSP_* env vars inject loss (lspnet.hpp).
 //   pipes: --miners N (default 1)  --devices d0,d1,.. (device of miner i =
@@ -51,7 +49,7 @@ namespace {
 // ----------------------------------------------------------------------------
 // LSP transport (server.go:83-168)
 // ----------------------------------------------------------------------------
-int run_lsp(int port, const lsp::Params& prm, uint64_t chunk, long exit_after, int hedge) {
+int run_lsp(int port, const lsp::Params& prm, uint64_t chunk, long exit_after) {
   std::string err;
   std::unique_ptr<lsp::Server> srv = lsp::NewServer(port, prm, &err);
   if (!srv) {
@@ -61,7 +59,6 @@ int run_lsp(int port, const lsp::Params& prm, uint64_t chunk, long exit_after, i
   printf("Server listening on port %d\n", srv->Port());
   fflush(stdout);
   sched::Scheduler S(chunk);
-  S.SetHedge(hedge);
   long answered = 0;
   for (;;) {
     int id = 0;
@@ -162,8 +159,7 @@ bool write_all(int fd, const std::string& s) {
 
 class PipeServer {
  public:
-  PipeServer(int nminers, std::vector<int> devs, uint64_t chunk, std::string cmd, int hedge) : S_(chunk) {
-    S_.SetHedge(hedge);
+  PipeServer(int nminers, std::vector<int> devs, uint64_t chunk, std::string cmd) : S_(chunk) {
     if (cmd.empty()) cmd = dir_of_self() + "/p1miner serve --device {dev}";
     for (int i = 0; i < nminers; ++i) {
       Child m;
@@ -240,9 +236,9 @@ class PipeServer {
 
 int usage() {
   fprintf(stderr,
-          "usage: p1server [--chunk C] [--hedge] [--epoch-limit K] [--epoch-millis M] [--window W] [--copies K] [--exit-after N] "
+          "usage: p1server [--chunk C] [--epoch-limit K] [--epoch-millis M] [--window W] [--copies K] [--exit-after N] "
           "lsp <port>\n"
-          "       p1server [--chunk C] [--hedge] [--miners N] [--devices d0,d1,..] [--miner-cmd CMD] "
+          "       p1server [--chunk C] [--miners N] [--devices d0,d1,..] [--miner-cmd CMD] "
           "scan <msg> <lower> <upper> | serve\n");
   return 2;
 }
@@ -269,7 +265,6 @@ int main(int argc, char** argv) {
   lsp::Params prm = lsp::NewParams();
   prm.Copies = lsp::DefaultAppCopies;
   long exit_after = 0;
-  int hedge = 1;
   int i = 1;
   for (; i < argc; ++i) {
     if (!strcmp(argv[i], "--miners") && i + 1 < argc) nminers = atoi(argv[++i]);
@@ -289,7 +284,6 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--window") && i + 1 < argc) prm.WindowSize = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--copies") && i + 1 < argc) prm.Copies = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--exit-after") && i + 1 < argc) exit_after = atol(argv[++i]);
-    else if (!strcmp(argv[i], "--hedge")) hedge = 2;
     else break;
   }
   if (i >= argc || nminers < 1 || prm.EpochLimit < 1 || prm.EpochMillis < 1 || prm.WindowSize < 1) return usage();
@@ -301,10 +295,10 @@ int main(int argc, char** argv) {
       printf("Port must be a number: %s\n", argv[i + 1]);  // server.go:68-72
       return 1;
     }
-    return run_lsp((int)port, prm, chunk, exit_after, hedge);
+    return run_lsp((int)port, prm, chunk, exit_after);
   }
   if (mode != "scan" && mode != "serve") return usage();
-  PipeServer srv(nminers, devs, chunk, cmd, hedge);
+  PipeServer srv(nminers, devs, chunk, cmd);
   if (srv.miners() == 0) { fprintf(stderr, "p1server: no miner started\n"); return 1; }
   if (mode == "scan" && i + 4 == argc) {
     uint64_t lo, hi;

@@ -23,14 +23,12 @@
 //   * a request's answer is the lexicographic (hash, nonce) min over its
 //     chunks with miner.go:56's identity (MaxUint64, 0) -- identical to one
 //     miner scanning the whole range (contiguous chunks, strict '<');
-//   * optional tail hedging (SetHedge(2), `p1server --hedge`): once no
-//     request has an unsent chunk, an idle miner gets a copy of the chunk
-//     that has been in flight longest (at most `copies` miners per chunk).
-//     The first Result for a chunk counts and later copies are ignored; a
-//     scan is deterministic, so every copy has the same answer.  Under loss
-//     a Request or Result datagram is only resent one LSP epoch later
-//     (2 s by default), which leaves a job waiting on one chunk while the
-//     other miners idle; a copy on an idle miner ends that wait.
+// (Round 3 had opt-in tail hedging -- idle miners running copies of the
+// chunks in flight longest -- against the one-epoch resend stall at 5% loss.
+// Sending each first transmission 3 times (lsp::Params::Copies) removed the
+// stall, after which hedging measured as a pure loss: 8 miners on one GPU,
+// configs[4], 2.64 s against 1.89 s median (profiles/r04b_lsp_m8c3h.json,
+// r04b_lsp_m8c3.json).  It was removed in round 4.)
 #pragma once
 #include <stdint.h>
 
@@ -86,15 +84,12 @@ class Scheduler {
     }
   }
 
-  // At most `copies` miners run one chunk (1 = no hedging, the default).
-  void SetHedge(int copies) { copies_ = copies < 1 ? 1 : copies; }
-
   void AddMiner(int miner) { miners_[miner]; }  // idle (server.go:153-166)
   bool IsMiner(int miner) const { return miners_.count(miner) != 0; }
   size_t Miners() const { return miners_.size(); }
 
-  // A miner is lost: its chunk goes back to the front of its request --
-  // unless another miner still runs a copy of it, or it is already answered.
+  // A miner is lost: its chunk goes back to the front of its request
+  // (unless the request is gone).
   void LoseMiner(int miner) {
     auto it = miners_.find(miner);
     if (it == miners_.end()) return;
@@ -104,12 +99,8 @@ class Scheduler {
       if (r != reqs_.end()) {
         auto f = r->second.inflight.find(m.lo);
         if (f != r->second.inflight.end()) {
-          if (f->second.copies > 1) {
-            f->second.copies--;
-          } else {
-            r->second.inflight.erase(f);
-            r->second.back.push_front({m.lo, m.hi});
-          }
+          r->second.inflight.erase(f);
+          r->second.back.push_front({m.lo, m.hi});
         }
       }
     }
@@ -127,7 +118,7 @@ class Scheduler {
     if (r == reqs_.end()) return true;  // its client is gone
     Req& q = r->second;
     auto f = q.inflight.find(m.lo);
-    if (f == q.inflight.end()) return true;  // a copy already answered this chunk
+    if (f == q.inflight.end()) return true;  // not (or no longer) outstanding
     q.inflight.erase(f);
     if (!q.has_work() && q.inflight.empty()) done_.push_back(q.id);
     // a chunk whose hashes are all MaxUint64 reports (Max, 0); only real
@@ -140,8 +131,7 @@ class Scheduler {
     return true;
   }
 
-  // Hand one chunk to every idle miner, round-robin over open requests;
-  // with hedging, idle miners left over get copies of the oldest chunks.
+  // Hand one chunk to every idle miner, round-robin over open requests.
   std::vector<Assignment> Dispatch() {
     std::vector<Assignment> out;
     for (auto& kv : miners_) {
@@ -154,12 +144,12 @@ class Scheduler {
         if (it == reqs_.end() || !it->second.has_work()) continue;
         Req& r = it->second;
         const Span c = r.take(chunk_);
-        r.inflight[c.lo] = {c.hi, 1, seq_++};
+        r.inflight[c.lo] = {c.hi};
         assign(kv.first, m, r, c.lo, c.hi, out);
         any = true;
         break;
       }
-      if (!any && !hedge_one(kv.first, m, out)) break;
+      if (!any) break;
     }
     return out;
   }
@@ -183,13 +173,11 @@ class Scheduler {
     return out;
   }
 
-  // Miners running a copy of the chunk of `req` that starts at `lo` (0 if
-  // none: unsent or answered).  Tests use it.
-  int Copies(uint64_t req, uint64_t lo) const {
+  // The chunk of `req` that starts at `lo` is out with a miner and not
+  // answered yet.  Tests use it.
+  bool InFlight(uint64_t req, uint64_t lo) const {
     auto it = reqs_.find(req);
-    if (it == reqs_.end()) return 0;
-    auto f = it->second.inflight.find(lo);
-    return f == it->second.inflight.end() ? 0 : f->second.copies;
+    return it != reqs_.end() && it->second.inflight.count(lo) != 0;
   }
 
   // Chunks a request still holds in memory (handed-back chunks; the unsent
@@ -207,10 +195,8 @@ class Scheduler {
   struct Span {
     uint64_t lo, hi;
   };
-  struct Flight {     // a chunk sent to at least one miner, not answered yet
+  struct Flight {     // a chunk sent to a miner, not answered yet
     uint64_t hi;
-    int copies;       // miners running it
-    uint64_t seq;     // dispatch order of its first copy (oldest is hedged first)
   };
   struct Req {
     uint64_t id;
@@ -249,26 +235,6 @@ class Scheduler {
     m.hi = hi;
     out.push_back({id, r.id, r.data, lo, hi});
   }
-  // Give idle miner `id` a copy of the oldest in-flight chunk that has fewer
-  // than copies_ miners; false if there is none (or hedging is off).
-  bool hedge_one(int id, Miner& m, std::vector<Assignment>& out) {
-    if (copies_ <= 1) return false;
-    Req* best_r = nullptr;
-    std::map<uint64_t, Flight>::iterator best_f;
-    for (auto& kv : reqs_) {
-      for (auto f = kv.second.inflight.begin(); f != kv.second.inflight.end(); ++f) {
-        if (f->second.copies >= copies_) continue;
-        if (!best_r || f->second.seq < best_f->second.seq) {
-          best_r = &kv.second;
-          best_f = f;
-        }
-      }
-    }
-    if (!best_r) return false;
-    best_f->second.copies++;
-    assign(id, m, *best_r, best_f->first, best_f->second.hi, out);
-    return true;
-  }
   void drop_order(uint64_t id) {
     for (size_t i = 0; i < order_.size(); ++i)
       if (order_[i] == id) {
@@ -284,8 +250,6 @@ class Scheduler {
   std::vector<uint64_t> done_;  // completed request ids, in completion order
   size_t rr_ = 0;
   uint64_t next_id_ = 1;
-  uint64_t seq_ = 0;
-  int copies_ = 1;
 };
 
 }  // namespace sched

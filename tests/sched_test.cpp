@@ -109,56 +109,24 @@ static void cancelled_client() {
   CHECK(S.Idle());
 }
 
-// Tail hedging: with no unsent chunk left, an idle miner runs a copy of the
-// oldest in-flight chunk; the first answer counts, the copy's is ignored.
-static void hedged_tail() {
+// A lost miner's in-flight chunk is re-queued at the front and goes to the
+// next idle miner.
+static void lost_chunk_in_flight() {
   sched::Scheduler S(10);
-  S.SetHedge(2);
-  const uint64_t id = S.Submit(1, "m", 0, 19);  // chunks [0,9], [10,19]
-  S.AddMiner(1);
-  S.AddMiner(2);
-  S.AddMiner(3);
-  auto a = S.Dispatch();
-  CHECK(a.size() == 3);  // two chunks + a copy of the oldest ([0,9])
-  CHECK(a[0].lo == 0 && a[1].lo == 10 && a[2].miner == 3 && a[2].lo == 0 && a[2].hi == 9);
-  CHECK(S.Copies(id, 0) == 2 && S.Copies(id, 10) == 1);
-  CHECK(S.Result(3, 7, 4));  // the copy answers [0,9] first
-  CHECK(S.Copies(id, 0) == 0);
-  a = S.Dispatch();  // miner 3 is idle again: a copy of [10,19], the only chunk left
-  CHECK(a.size() == 1 && a[0].miner == 3 && a[0].lo == 10);
-  CHECK(S.Result(1, 1, 1));  // miner 1's late answer for [0,9] is ignored
-  CHECK(S.TakeDone().empty());
-  CHECK(S.Result(2, 6, 15));  // [10,19] answered by its first miner
-  auto d = S.TakeDone();
-  CHECK(d.size() == 1 && d[0].req == id && d[0].hash == 6 && d[0].nonce == 15);
-  CHECK(S.Result(3, 6, 15));  // the copy's answer for a finished request is absorbed
-  CHECK(S.Idle());
-  // without hedging the third miner stays idle
-  sched::Scheduler T(10);
-  T.Submit(1, "m", 0, 19);
-  T.AddMiner(1);
-  T.AddMiner(2);
-  T.AddMiner(3);
-  CHECK(T.Dispatch().size() == 2);
-}
-
-// A lost miner's chunk is re-queued only if no other copy still runs.
-static void hedged_loss() {
-  sched::Scheduler S(10);
-  S.SetHedge(2);
-  const uint64_t id = S.Submit(1, "m", 0, 9);
+  const uint64_t id = S.Submit(1, "m", 0, 19);
   S.AddMiner(1);
   S.AddMiner(2);
   auto a = S.Dispatch();
-  CHECK(a.size() == 2 && a[0].lo == 0 && a[1].lo == 0);  // the chunk and its copy
+  CHECK(a.size() == 2 && a[0].lo == 0 && a[1].lo == 10);
+  CHECK(S.InFlight(id, 0) && S.InFlight(id, 10));
   S.LoseMiner(1);
-  CHECK(S.Copies(id, 0) == 1 && S.HeldSpans(id) == 0);  // miner 2's copy still runs
-  S.LoseMiner(2);
-  CHECK(S.Copies(id, 0) == 0 && S.HeldSpans(id) == 1);  // no copy left: re-queued
-  S.AddMiner(3);
+  CHECK(!S.InFlight(id, 0) && S.HeldSpans(id) == 1);
+  CHECK(S.Dispatch().empty());  // miner 2 is still busy
+  CHECK(S.Result(2, 9, 12));
   a = S.Dispatch();
-  CHECK(a.size() == 1 && a[0].miner == 3 && a[0].lo == 0 && a[0].hi == 9);
-  CHECK(S.Result(3, 2, 3));
+  CHECK(a.size() == 1 && a[0].miner == 2 && a[0].lo == 0 && a[0].hi == 9);
+  CHECK(S.Result(2, 2, 3));
+  CHECK(S.Result(2, 1, 1) == false);  // a stray Result from an idle miner is ignored
   auto d = S.TakeDone();
   CHECK(d.size() == 1 && d[0].hash == 2 && d[0].nonce == 3);
 }
@@ -169,8 +137,7 @@ int main() {
   answer_and_identity();
   completion_order();
   cancelled_client();
-  hedged_tail();
-  hedged_loss();
+  lost_chunk_in_flight();
   printf("sched_test: ok\n");
   return 0;
 }

@@ -322,19 +322,20 @@ def test_client_does_not_spin_after_server_dies(system):
         p.wait()
 
 
-@pytest.mark.parametrize("hedge", ["0", "1"])
-def test_bench_lsp_plumbing_with_cpu_miners(oracle_mod, hedge):
+@pytest.mark.parametrize("copies", ["1", "3"])
+def test_bench_lsp_plumbing_with_cpu_miners(oracle_mod, copies):
     """tools/bench_lsp.py (configs[4] end to end over LSP) with the CPU miner
-    doubles: server (with and without tail hedging), 3 miners, window 8, 5%
-    drop, short epochs; the timed requests agree with each other and with
+    doubles: server, 3 miners, window 8, 5% drop, short epochs, the
+    reference protocol (1 copy) and the programs' default (3 copies per
+    first transmission); the timed requests agree with each other and with
     the oracle."""
     import json
 
     env = dict(os.environ, FAKE="1", MINERS="3", UPPER="99999", CHUNK="20000", REPS="2", EPOCH_MS="100",
-               HEDGE=hedge)
+               COPIES=copies)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_lsp.py")], capture_output=True,
                        text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout)
     assert d["consistent"] and tuple(d["result"]) == oracle_mod.scan("bradfitz", 0, 99999)
-    assert d["reps"] == 2 and len(d["wall_s"]) == 2
+    assert d["reps"] == 2 and len(d["wall_s"]) == 2 and d["copies"] == int(copies)

@@ -10,8 +10,7 @@ the system's overhead on top of one GPU, not an 8-GPU rate.
 env: MINERS (8), NGPU (1), UPPER (2^36 - 1), CHUNK (2^32), WINDOW (8),
      DROP (5), REPS (3), EPOCH_MS (unset: the reference's 2000 ms epochs;
      a lost datagram is resent one epoch later, so at 5% drop the wall time
-     holds whole epochs), HEDGE=1 (p1server --hedge: idle miners run copies
-     of the chunks in flight longest), COPIES (unset: the programs' default,
+     holds whole epochs), COPIES (unset: the programs' default,
      lsp::DefaultAppCopies = 3; 1 = the reference protocol: datagrams per
      first transmission); FAKE=1 runs the CPU oracle-backed miner double
      (tools/lsp_fake_miner, test plumbing only) instead of p1miner
@@ -56,8 +55,7 @@ def main():
         lsp += ["--copies", copies]
     procs = []
     try:
-        hedge = os.environ.get("HEDGE") == "1"
-        srv = subprocess.Popen([SERVER, "--chunk", str(chunk)] + (["--hedge"] if hedge else []) + lsp + ["lsp", "0"],
+        srv = subprocess.Popen([SERVER, "--chunk", str(chunk)] + lsp + ["lsp", "0"],
                                stdout=subprocess.PIPE, text=True, env=env)
         procs.append(srv)
         line = srv.stdout.readline()
@@ -96,7 +94,7 @@ def main():
             "workload": f"configs[4]: client 'bradfitz' maxNonce {upper} -> p1server lsp (chunks of {chunk}) -> "
                         f"{miners} {'CPU oracle miner doubles' if fake else f'p1miner lsp processes on {ngpu} GPU(s)'}"
                         f"; LSP window {window}, {drop}% write drop in every process, "
-                        f"{epoch or 'default (2000)'} ms epochs{', tail hedging' if hedge else ''}, "
+                        f"{epoch or 'default (2000)'} ms epochs, "
                         f"{copies or 'default (3)'} copies per first transmission",
             "copies": int(copies) if copies else 3, "epoch_ms": int(epoch) if epoch else 2000, "miners": miners,
             "reps": reps, "wall_s": walls, "wall_s_median": med, "warmup_wall_s": warm_s,
