@@ -408,6 +408,13 @@ def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof
         "kernel_hashes_per_s_G": k_rate / 1e9,
         "fast_nonce_share": stats["fast_nonces"] / max(1, stats["fast_nonces"] + stats["generic_nonces"]),
     }
+    if pmc and pmc.get("write_bytes_per_launch_calibrated") is not None:
+        # WRITE_SIZE counts k_scan's 16-B-per-workgroup partial stores 2x
+        # (profiles/r04c_wcal.json): the calibrated bytes against the
+        # algorithmic ones (16 B per workgroup)
+        roof["traffic_calibrated"] = pmc["write_bytes_per_launch_calibrated"] + pmc.get("fetch_bytes_per_launch", 0.0)
+        roof["alg_bytes_per_launch"] = pmc.get("partials_bytes_per_launch")
+        roof["traffic_note"] = pmc.get("traffic_note")
     avg_ns, src = rocprof
     if single_gpu and avg_ns and k_n:
         # one launch of this config's plan; rocprofv3 --kernel-trace average
