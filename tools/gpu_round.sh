@@ -28,6 +28,16 @@ for cfg in ${BENCH_CONFIGS:-}; do
 done
 [ "${RUN_SWEEP:-0}" != 1 ] || step sweep 900 python "$ROOT/tools/sweep.py" > "$OUT/${TAG}_sweep.jsonl" 2> "$OUT/${TAG}_sweep.err"
 [ "${RUN_SERVER:-0}" != 1 ] || step bench_server 900 python "$ROOT/tools/bench_server.py" > "$OUT/${TAG}_bench_server.json" 2> "$OUT/${TAG}_bench_server.err"
+if [ "${RUN_STRESS:-0}" = 1 ]; then
+  # randomized parity against the oracle: production settings, then the
+  # fast variants forced onto small ranges (test knobs under their switch)
+  step stress 300 python "$ROOT/tools/stress.py" ${STRESS_S:-150} > "$OUT/${TAG}_stress.json" 2> "$OUT/${TAG}_stress.err"
+  P1HIP_TEST_KNOBS=1 P1HIP_MIN_FAST_THREADS=1 P1HIP_SMALL_MAX_NONCES=0 step stress_k3 300 python "$ROOT/tools/stress.py" ${STRESS_S:-150} 441 > "$OUT/${TAG}_stress_k3.json" 2> "$OUT/${TAG}_stress_k3.err"
+fi
+if [ "${RUN_TORCHRUN8:-0}" = 1 ]; then
+  # the driver's N = 8 launch shape on one GPU: 8 ranks, gloo all-gather
+  step torchrun8 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29513 "$ROOT/bench.py" --gpus 8 --steps 2 --warmup 1 --dist-backend gloo > "$OUT/${TAG}_torchrun8.json" 2> "$OUT/${TAG}_torchrun8.err"
+fi
 if [ "${RUN_TORCHRUN:-0}" = 1 ]; then
   # rehearse the N>1 launch path on one GPU: 2 ranks, gloo all-gather, shared device
   step torchrun2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 "$ROOT/bench.py" --gpus 2 --steps 2 --warmup 1 --dist-backend gloo > "$OUT/${TAG}_torchrun2.json" 2> "$OUT/${TAG}_torchrun2.err"

@@ -10,6 +10,9 @@ production settings (one-launch small path, MODE 5 tables, default occupancy
 floor).  Prints one JSON summary line.
 
 usage: [STRESS_MAXLEN=n] python tools/stress.py [seconds] [seed]
+(the fast-variant run forces k = 3 on small ranges with the test knobs
+P1HIP_TEST_KNOBS=1 P1HIP_MIN_FAST_THREADS=1 P1HIP_SMALL_MAX_NONCES=0; the
+summary line records the knobs in force)
 """
 import json
 import os
@@ -74,7 +77,8 @@ def main():
             if not ok:
                 fails.append({"msg_hex": m.hex(), "lower": lo, "upper": hi, "got": got})
     print(json.dumps({"seed": seed, "seconds": secs, "requests_exact": n_exact, "requests_property": n_prop,
-                      "nonces_scanned": nonces, "failures": fails[:20], "n_failures": len(fails)}), flush=True)
+                      "nonces_scanned": nonces, "failures": fails[:20], "n_failures": len(fails),
+                      "test_knobs": p1_amd.test_knobs(), "library": p1_amd.version()}), flush=True)
     sys.exit(1 if fails else 0)
 
 
