@@ -476,6 +476,30 @@ def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof
     return roof
 
 
+SHARD_BALANCE_PROFILE = "profiles/r03h_shard_balance.jsonl"
+
+
+def scaling_expectation(config, n):
+    """What an N-GPU c4 run should reach if every GPU runs like the one the
+    shards were measured on: 2^38 / the slowest plan_shards shard, each shard
+    timed alone on one GPU (tools/shard_balance.py).  None for other configs
+    or N without a measurement."""
+    if config != "c4" or n < 2:
+        return None
+    try:
+        with open(os.path.join(ROOT, SHARD_BALANCE_PROFILE)) as f:
+            for line in f:
+                d = json.loads(line)
+                if d.get("n") == n and d.get("split") == "plan_shards":
+                    return {"implied_GH_s": d["implied_GH_s"], "slowest_shard_over_mean": d["max_over_mean"],
+                            "shard_kernel_ms": d["kernel_ms"], "source": SHARD_BALANCE_PROFILE,
+                            "note": "2^38 / the slowest of this N's plan_shards shards, each timed alone on "
+                                    "one GPU; a shortfall against it is cross-GPU (see per_gpu)"}
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
 def device_identity(index):
     """Ordinal, PCI bus id, UUID, arch and host of a device the library
     opened (p1hip_device_info), for the per-GPU records."""
@@ -741,6 +765,7 @@ def main():
             "test_knobs": knobs,
             "library": {"path": os.path.relpath(p1_amd.lib_path(), ROOT), "version": p1_amd.version()},
             "topology": topology,
+            "scaling_expectation": scaling_expectation(run["config"], n_gpus),
             "roofline": roofline,
             "per_gpu": scaling_report(units, args.steps, ms_per_step),
             "result": {"hash": result[0], "nonce": result[1], "consistent": consistent,

@@ -192,3 +192,11 @@ def test_bench_imports_torch_before_the_library():
 
     src = inspect.getsource(bench.main)
     assert src.index("import torch\n") < src.index("import p1_amd\n")
+
+
+def test_scaling_expectation_for_the_driver_shapes():
+    for n in (2, 4, 8):
+        e = bench.scaling_expectation("c4", n)
+        assert e and e["slowest_shard_over_mean"] < 1.01 and len(e["shard_kernel_ms"]) == n
+    assert 290 < bench.scaling_expectation("c4", 8)["implied_GH_s"] < 300
+    assert bench.scaling_expectation("c4", 1) is None and bench.scaling_expectation("c2", 8) is None
