@@ -97,7 +97,8 @@ def main():
                         f"{epoch or 'default (2000)'} ms epochs, "
                         f"{copies or 'default (3)'} copies per first transmission",
             "copies": int(copies) if copies else 3, "epoch_ms": int(epoch) if epoch else 2000, "miners": miners,
-            "reps": reps, "wall_s": walls, "wall_s_median": med, "warmup_wall_s": warm_s,
+            "reps": reps, "wall_s": walls, "wall_s_median": med, "wall_s_max": max(walls),
+            "wall_s_p90": sorted(walls)[min(len(walls) - 1, int(0.9 * len(walls)))], "warmup_wall_s": warm_s,
             "GH_s": (upper + 1) / med / 1e9,
             "result": results[-1], "consistent": all(r == results[0] for r in results),
             "matches_known": (results[-1] == want) if want else None}), flush=True)
