@@ -21,7 +21,7 @@ ISAPOST ?= --align-loops=3 --loop-offset=4 --loop-parity
 BUILD := build
 
 all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios \
-     tools/lsp_fake_miner tools/queue_ctl tools/wcal
+     tools/lsp_fake_miner tools/queue_ctl tools/wcal tools/vbank
 
 $(BUILD)/p1hip_kernels.s: $(CSRC)/p1hip_kernels.hip $(DEVHDRS) Makefile
 	mkdir -p $(BUILD)
@@ -80,6 +80,10 @@ tools/queue_ctl: tools/queue_ctl.cpp include/p1hip.h p1_amd/libp1hip.so
 tools/wcal: tools/wcal.hip
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -o $@ tools/wcal.hip
 
+# measurement program: VALU issue cost vs operand VGPR banks
+tools/vbank: tools/vbank.hip
+	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -o $@ tools/vbank.hip
+
 # host-only replay of the kernels' per-thread code (layout tests; not product)
 tools/p1emu: tools/p1emu.cpp $(HDRS)
 	$(HIPCC) -O2 -std=c++17 -DP1_NV2_PLAIN -o $@ tools/p1emu.cpp
@@ -101,7 +105,7 @@ isa: $(BUILD)/p1hip_kernels.post.s
 	$(HIPCC) $(DEVFLAGS) -c -o /dev/null $(CSRC)/p1hip_kernels.hip -Rpass-analysis=kernel-resource-usage 2> $(BUILD)/resource.txt || true
 
 clean:
-	rm -f p1_amd/libp1hip.so tools/queue_ctl tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios tools/lsp_fake_miner tools/wcal
+	rm -f p1_amd/libp1hip.so tools/queue_ctl tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios tools/lsp_fake_miner tools/wcal tools/vbank
 	rm -rf $(BUILD)/p1hip_kernels* $(BUILD)/p1hip_host.o
 	$(MAKE) -C oracle clean
 .PHONY: all oracle clean isa variant
