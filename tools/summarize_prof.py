@@ -79,6 +79,7 @@ def main():
     for f in glob.glob(os.path.join(src, f"{tag}_bench*.json")) + glob.glob(os.path.join(src, f"{tag}_valu_*.jsonl")):
         shutil.copy(f, os.path.join(dst, os.path.basename(f)))
     counters, durs, sums = {}, [], {}
+    gmax_all = 0  # largest k_scan grid (threads) seen in the PMC passes
     for f in sorted(glob.glob(os.path.join(src, f"{tag}_pmc*", "*counter_collection.csv"))):
         rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].split("(")[0] == "k_scan"]
         if not rows:
@@ -86,6 +87,7 @@ def main():
         # only the workload's own launches (largest grid); bench.py also times
         # small configs[0]-sized requests whose launches are not the roofline kernel
         gmax = max(int(r["Grid_Size"]) for r in rows)
+        gmax_all = max(gmax_all, gmax)
         for r in rows:
             sums[r["Counter_Name"]] = sums.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
             if int(r["Grid_Size"]) != gmax:
@@ -137,6 +139,22 @@ def main():
         # (MI355X_MICROARCH.md HBM section) -- this kernel has no such reads (kernel args,
         # a <4 KB segment table via scalar loads, 16-B partial stores), so no correction applies.
         out["hbm_bytes_per_launch"] = (avg.get("FETCH_SIZE", 0.0) + avg.get("WRITE_SIZE", 0.0)) * 1024
+        out["fetch_bytes_per_launch"] = avg.get("FETCH_SIZE", 0.0) * 1024
+        out["write_bytes_per_launch"] = avg.get("WRITE_SIZE", 0.0) * 1024
+        # k_scan stores one 16-B partial per 256-thread workgroup; the
+        # calibration kernel of the same pattern (tools/wcal.hip) gives the
+        # factor WRITE_SIZE counts it with (profiles/*_wcal.json)
+        cal = sorted(glob.glob(os.path.join(dst, "*_wcal.json")))
+        if cal and "WRITE_SIZE" in avg:
+            c = json.load(open(cal[-1]))
+            factor = c["k_part16"]["counted_over_actual"]
+            out["write_bytes_per_launch_calibrated"] = out["write_bytes_per_launch"] / factor
+            out["partials_bytes_per_launch"] = gmax_all / 256 * 16
+            out["traffic_note"] = (f"raw FETCH_SIZE+WRITE_SIZE per k_scan launch; WRITE_SIZE counts k_scan's "
+                                   f"16-B-per-workgroup partial stores {factor:.2f}x "
+                                   f"({os.path.relpath(cal[-1], ROOT)}), so the calibrated write bytes are "
+                                   f"write_bytes_per_launch_calibrated against partials_bytes_per_launch "
+                                   f"(16 B x workgroups); FETCH is kernel arguments and segment tables")
     with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
