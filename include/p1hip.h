@@ -173,9 +173,11 @@ const char *p1hip_version(void);
  * caps, combine mode ...) only while the master switch P1HIP_TEST_KNOBS=1 is
  * set in the environment; otherwise they are ignored and this returns "".
  * With the switch set it returns "P1HIP_TEST_KNOBS=1" followed by
- * ";NAME=value" for every knob that is set.  bench.py refuses to time a run
- * for which this is not "".  The string is per thread and valid until the
- * next call from that thread. */
+ * ";NAME=value" for every knob that is set; knobs read at init that the open
+ * devices still run with are listed too ("NAME=(init: value)"), even if the
+ * environment changed since.  bench.py refuses to time a run for which this
+ * is not "".  The string is per thread and valid until the next call from
+ * that thread. */
 const char *p1hip_test_knobs(void);
 
 /* Release streams, buffers and communicators.  Safe to call twice. */

@@ -215,7 +215,7 @@ def test_knobs():
     """The library's test knobs in force for this process, as a dict ({} in
     production: the knobs are honoured only under P1HIP_TEST_KNOBS=1)."""
     raw = load().p1hip_test_knobs().decode()
-    return dict(kv.split("=", 1) for kv in raw.split(";") if kv)
+    return dict(kv.split("=", 1) if "=" in kv else (kv, "?") for kv in raw.split(";") if kv)
 
 
 def reset_stats():

@@ -978,10 +978,38 @@ const char* p1hip_version(void) { return "p1hip 0.4 gfx950"; }
 const char* p1hip_test_knobs(void) {
   static thread_local std::string s;
   s.clear();
-  if (!test_knobs_on()) return s.c_str();
-  s = "P1HIP_TEST_KNOBS=1";
-  for (const char* k : kTestKnobs)
-    if (const char* v = test_knob(k)) s += std::string(";") + k + "=" + v;
+  try {
+    // the knobs the environment sets now (read per scan, or at the next init)
+    std::vector<std::pair<std::string, std::string>> kv;
+    if (test_knobs_on()) {
+      kv.push_back({"P1HIP_TEST_KNOBS", "1"});
+      for (const char* k : kTestKnobs)
+        if (const char* v = test_knob(k)) kv.push_back({k, v});
+    }
+    // ... and the ones read at init that the open devices still run with,
+    // even if the environment has changed since
+    Runtime& R = rt();
+    std::lock_guard<std::mutex> g(R.mu);
+    auto add = [&](const char* k, const std::string& v) {
+      for (auto& e : kv)
+        if (e.first == k) {
+          if (e.second != v) e.second += " (init: " + v + ")";
+          return;
+        }
+      kv.push_back({k, "(init: " + v + ")"});
+    };
+    if (!R.devs.empty()) {
+      if (R.min_fast_threads != kMinFastThreads) add("P1HIP_MIN_FAST_THREADS", std::to_string(R.min_fast_threads));
+      if (R.fail_device >= 0) add("P1HIP_TEST_FAIL_DEVICE", std::to_string(R.fail_device));
+      if (!R.tabulate) add("P1HIP_NO_TABLE", "1");
+      if (!R.split) add("P1HIP_NO_SPLIT", "1");
+      if (!R.use_rccl) add("P1HIP_NO_RCCL", "1");
+      if (R.rccl_one) add("P1HIP_FORCE_RCCL", "1");
+    }
+    for (size_t i = 0; i < kv.size(); ++i) s += (i ? ";" : "") + kv[i].first + "=" + kv[i].second;
+  } catch (...) {
+    s = "?";  // never empty when the state could not be read
+  }
   return s.c_str();
 }
 

@@ -307,7 +307,7 @@ def test_failure_on_one_device_does_not_hang(reinit, oracle_mod):
     assert g.scan("bradfitz", 0, 9999) == (1419516646206828, 9898)
 
 
-def test_test_knobs_are_fenced_off_production(reinit):
+def test_test_knobs_are_fenced_off_production(reinit, monkeypatch):
     """a stray test knob in a production environment
     changes nothing.  P1HIP_TEST_FAIL_DEVICE=0 without the master switch
     P1HIP_TEST_KNOBS=1 is ignored (the scan succeeds and p1hip_test_knobs()
@@ -320,6 +320,13 @@ def test_test_knobs_are_fenced_off_production(reinit):
     with pytest.raises(g.P1HipError) as e:
         g.scan("bradfitz", 0, 99999)
     assert e.value.rc == -2 and "injected" in str(e.value)
+    # a knob read at init stays reported while the devices run with it, even
+    # after the environment dropped it
+    g = reinit(P1HIP_TEST_FAIL_DEVICE=-1, P1HIP_MIN_FAST_THREADS=1)
+    monkeypatch.delenv("P1HIP_MIN_FAST_THREADS")
+    monkeypatch.setenv("P1HIP_TEST_KNOBS", "0")
+    assert g.test_knobs() == {"P1HIP_MIN_FAST_THREADS": "(init: 1)"}
+    monkeypatch.setenv("P1HIP_TEST_KNOBS", "1")
     g = reinit(P1HIP_TEST_FAIL_DEVICE=-1)
 
 
