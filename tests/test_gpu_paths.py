@@ -315,6 +315,7 @@ def test_test_knobs_are_fenced_off_production(reinit, monkeypatch):
     g = reinit(P1HIP_TEST_KNOBS=0, P1HIP_TEST_FAIL_DEVICE=0, P1HIP_NO_TABLE=1)
     assert g.test_knobs() == {}
     assert g.scan("bradfitz", 0, 99999) == (85364550342847, 98985)  # = oracle
+    monkeypatch.delenv("P1HIP_NO_TABLE")
     g = reinit(P1HIP_TEST_KNOBS=1, P1HIP_TEST_FAIL_DEVICE=0)
     assert g.test_knobs()["P1HIP_TEST_FAIL_DEVICE"] == "0"
     with pytest.raises(g.P1HipError) as e:
