@@ -91,6 +91,42 @@ tools/p1emu: tools/p1emu.cpp $(HDRS)
 oracle:
 	$(MAKE) -C oracle
 
+# Host code under sanitizers (tools/sanitize.sh, tests/test_sanitizers.py):
+# ASan + UBSan (no recovery) and TSan builds of the LSP stack, the server
+# scheduler, the client, the CPU test-double miner and the planner replay.
+# ROCm's clang: its TSan intercepts pthread_cond_clockwait, which libstdc++
+# uses for steady_clock waits and GCC 11's TSan does not (every condition
+# wait then reads as a double lock).  p1emu includes the HIP headers, so it
+# goes through hipcc with the sanitizers on the host side only.
+SANCXX ?= /opt/rocm/lib/llvm/bin/clang++
+SANBASE := -O1 -g -std=c++17 -pthread -fno-omit-frame-pointer
+SAN_asan := -fsanitize=address,undefined -fno-sanitize-recover=undefined
+SAN_tsan := -fsanitize=thread
+SANDIR := $(BUILD)/san
+SANPROGS := lsp_scenarios sched_test p1server p1client lsp_fake_miner
+sanitize: $(foreach s,asan tsan,$(addprefix $(SANDIR)/$(s)/,$(SANPROGS)))
+sanitize-emu: $(SANDIR)/asan/p1emu
+
+$(SANDIR)/%/lsp_scenarios: tests/lsp/lsp_scenarios.cpp p1_amd/host/lsp.cpp p1_amd/host/lspnet.cpp p1_amd/host/lsp_message.cpp $(HOSTHDR)
+	mkdir -p $(@D)
+	$(SANCXX) $(SANBASE) $(SAN_$*) -o $@ tests/lsp/lsp_scenarios.cpp p1_amd/host/lsp.cpp p1_amd/host/lspnet.cpp p1_amd/host/lsp_message.cpp
+$(SANDIR)/%/sched_test: tests/sched_test.cpp p1_amd/host/scheduler.hpp
+	mkdir -p $(@D)
+	$(SANCXX) $(SANBASE) $(SAN_$*) -o $@ tests/sched_test.cpp
+$(SANDIR)/%/p1server: p1_amd/host/p1server.cpp $(HOSTSRC) $(HOSTHDR)
+	mkdir -p $(@D)
+	$(SANCXX) $(SANBASE) $(SAN_$*) -o $@ p1_amd/host/p1server.cpp $(HOSTSRC)
+$(SANDIR)/%/p1client: p1_amd/host/p1client.cpp $(HOSTSRC) $(HOSTHDR)
+	mkdir -p $(@D)
+	$(SANCXX) $(SANBASE) $(SAN_$*) -o $@ p1_amd/host/p1client.cpp $(HOSTSRC)
+$(SANDIR)/%/lsp_fake_miner: tests/lsp/lsp_fake_miner.cpp $(HOSTSRC) $(HOSTHDR) oracle
+	mkdir -p $(@D)
+	$(SANCXX) $(SANBASE) $(SAN_$*) -o $@ tests/lsp/lsp_fake_miner.cpp $(HOSTSRC) -L$(CURDIR)/oracle -lp1oracle -Wl,-rpath,$(CURDIR)/oracle
+$(SANDIR)/asan/p1emu: tools/p1emu.cpp $(HDRS)
+	mkdir -p $(@D)
+	$(HIPCC) -O1 -g -std=c++17 -fno-omit-frame-pointer -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+	    -Xarch_host -fno-sanitize-recover=undefined -DP1_NV2_PLAIN -o $@ tools/p1emu.cpp
+
 # A/B tuning builds (not used unless P1HIP_LIB points at one):
 #   make variant NAME=x DEVEXTRA='-DP1_FAST_WAVES=5' ISAPOST='--no-e64'
 #   make variant NAME=nv2 DEVEXTRA=-DP1_NV2_PLAIN HOSTEXTRA=-DP1_NV2_PLAIN   (+ P1HIP_NO_SPLIT=1 at run time)
@@ -108,4 +144,4 @@ clean:
 	rm -f p1_amd/libp1hip.so tools/queue_ctl tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios tools/lsp_fake_miner tools/wcal tools/vbank
 	rm -rf $(BUILD)/p1hip_kernels* $(BUILD)/p1hip_host.o
 	$(MAKE) -C oracle clean
-.PHONY: all oracle clean isa variant
+.PHONY: all oracle clean isa variant sanitize sanitize-emu

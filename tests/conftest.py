@@ -9,6 +9,18 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def host_bin(path):
+    """A host program's path, or its sanitizer build when P1_SAN_DIR names
+    one (`make sanitize`: build/san/asan, build/san/tsan; tools/sanitize.sh
+    re-runs the host-program tests against those)."""
+    san = os.environ.get("P1_SAN_DIR")
+    if san:
+        alt = os.path.join(san, os.path.basename(path))
+        if os.path.exists(alt):
+            return alt
+    return path
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box)")
     # a fresh checkout builds once (normally everything is prebuilt by `make`)

@@ -9,10 +9,10 @@ import subprocess
 
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, host_bin
 
 U64_MAX = (1 << 64) - 1
-EMU = os.path.join(ROOT, "tools", "p1emu")
+EMU = host_bin(os.path.join(ROOT, "tools", "p1emu"))
 
 
 def emu(msg, lo, hi, generic=False, minthreads=None, nosplit=False, variants=None, notable=False):

@@ -16,9 +16,9 @@ import subprocess
 
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, host_bin
 
-DRIVER = os.path.join(ROOT, "tools", "lsp_scenarios")
+DRIVER = host_bin(os.path.join(ROOT, "tools", "lsp_scenarios"))
 
 SCENARIOS = [f"Basic{i}" for i in range(1, 10)] + [f"SendReceive{i}" for i in range(1, 4)] + \
     [f"Robust{i}" for i in range(1, 7)] + [f"Window{i}" for i in range(1, 7)] + \

@@ -14,12 +14,12 @@ import time
 
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, host_bin
 
-SERVER = os.path.join(ROOT, "p1_amd", "p1server")
-CLIENT = os.path.join(ROOT, "p1_amd", "p1client")
+SERVER = host_bin(os.path.join(ROOT, "p1_amd", "p1server"))
+CLIENT = host_bin(os.path.join(ROOT, "p1_amd", "p1client"))
 MINER = os.path.join(ROOT, "p1_amd", "p1miner")
-FAKE = os.path.join(ROOT, "tools", "lsp_fake_miner")
+FAKE = host_bin(os.path.join(ROOT, "tools", "lsp_fake_miner"))
 
 
 def kfd_queues(pid):

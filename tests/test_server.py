@@ -9,9 +9,9 @@ import subprocess
 
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, host_bin
 
-SERVER = os.path.join(ROOT, "p1_amd", "p1server")
+SERVER = host_bin(os.path.join(ROOT, "p1_amd", "p1server"))
 FAKE = f"python3 {os.path.join(ROOT, 'tests', 'fake_miner.py')}"
 U64_MAX = (1 << 64) - 1
 
