@@ -122,6 +122,21 @@ $(SANDIR)/%/p1client: p1_amd/host/p1client.cpp $(HOSTSRC) $(HOSTHDR)
 $(SANDIR)/%/lsp_fake_miner: tests/lsp/lsp_fake_miner.cpp $(HOSTSRC) $(HOSTHDR) oracle
 	mkdir -p $(@D)
 	$(SANCXX) $(SANBASE) $(SAN_$*) -o $@ tests/lsp/lsp_fake_miner.cpp $(HOSTSRC) -L$(CURDIR)/oracle -lp1oracle -Wl,-rpath,$(CURDIR)/oracle
+# the library's host runtime under ASan + UBSan (host side only: the kernels
+# are the shipped code object) and its GPU stress driver; in tools/san, not
+# build/, so that they travel to the GPU box with the tree
+SANLIB := tools/san
+sanitize-lib: $(SANLIB)/libp1hip.so $(SANLIB)/capi_san_stress
+$(SANLIB)/p1hip_host.o: $(CSRC)/p1hip.hip $(HDRS)
+	mkdir -p $(@D)
+	$(HIPCC) -O1 -g -std=c++17 -fPIC --offload-arch=$(ARCH) -fno-omit-frame-pointer -Xarch_host -fsanitize=address \
+	    -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined -c -o $@ $(CSRC)/p1hip.hip
+$(SANLIB)/libp1hip.so: $(SANLIB)/p1hip_host.o $(BUILD)/p1hip_kernels_blob.o
+	$(HIPCC) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+$(SANLIB)/capi_san_stress: tests/capi_san_stress.cpp include/p1hip.h $(SANLIB)/libp1hip.so oracle
+	$(SANCXX) $(SANBASE) $(SAN_asan) -Iinclude -o $@ tests/capi_san_stress.cpp -L$(SANLIB) -lp1hip \
+	    -Wl,-rpath,'$$ORIGIN' -Loracle -lp1oracle -Wl,-rpath,'$$ORIGIN/../../oracle'
+
 $(SANDIR)/asan/p1emu: tools/p1emu.cpp $(HDRS)
 	mkdir -p $(@D)
 	$(HIPCC) -O1 -g -std=c++17 -fno-omit-frame-pointer -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
@@ -144,4 +159,4 @@ clean:
 	rm -f p1_amd/libp1hip.so tools/queue_ctl tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios tools/lsp_fake_miner tools/wcal tools/vbank
 	rm -rf $(BUILD)/p1hip_kernels* $(BUILD)/p1hip_host.o
 	$(MAKE) -C oracle clean
-.PHONY: all oracle clean isa variant sanitize sanitize-emu
+.PHONY: all oracle clean isa variant sanitize sanitize-emu sanitize-lib

@@ -87,3 +87,31 @@ def test_chunkloop_on_gpu(tmp_path, oracle_mod):
         assert r.stdout.split()[:3] == ["Result", str(want[0]), str(want[1])], (msg, r.stdout)
         if (hi - lo + 1) // chunk >= 3:
             assert "cpu_chunks=0" not in r.stdout
+
+
+SAN_STRESS = os.path.join(ROOT, "tools", "san", "capi_san_stress")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(SAN_STRESS), reason="`make sanitize-lib` not built (ASan host runtime)")
+def test_host_runtime_under_asan(tmp_path):
+    """The library's host runtime built with ASan + UBSan on the host side
+    (`make sanitize-lib`; the kernels are the shipped code object) drives
+    real scans for 40 s: planner, argument errors, exact and property-checked
+    random scans, 4 host threads at once, the argmin on crafted pairs, 3
+    logical devices with host combine, launch / table / span caps, an
+    injected device failure and recovery, re-init cycles
+    (tests/capi_san_stress.cpp).  Passes only with rc 0 and no report file."""
+    env = dict(os.environ,
+               ASAN_OPTIONS=f"detect_leaks=1:log_path={tmp_path}/asan",
+               LSAN_OPTIONS=f"suppressions={os.path.join(ROOT, 'tests', 'lsan_rocm.supp')}",
+               UBSAN_OPTIONS=f"print_stacktrace=1:halt_on_error=1:log_path={tmp_path}/ubsan")
+    for k in list(env):
+        if k.startswith("P1HIP_"):
+            del env[k]
+    r = subprocess.run([SAN_STRESS, "40"], capture_output=True, text=True, timeout=110, env=env)
+    reports = sorted(f for f in os.listdir(tmp_path) if f.split(".")[0] in ("asan", "ubsan"))
+    text = "".join(open(os.path.join(tmp_path, f)).read()[:4000] for f in reports)
+    print(r.stdout)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr + text
+    assert not reports, text
