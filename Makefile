@@ -137,6 +137,19 @@ $(SANLIB)/capi_san_stress: tests/capi_san_stress.cpp include/p1hip.h $(SANLIB)/l
 	$(SANCXX) $(SANBASE) $(SAN_asan) -Iinclude -o $@ tests/capi_san_stress.cpp -L$(SANLIB) -lp1hip \
 	    -Wl,-rpath,'$$ORIGIN' -Loracle -lp1oracle -Wl,-rpath,'$$ORIGIN/../../oracle'
 
+# the same under TSan (the device threads, barriers and the combine of a
+# multi-device scan; the HIP runtime itself is not instrumented)
+sanitize-lib-tsan: $(SANLIB)/tsan/libp1hip.so $(SANLIB)/tsan/capi_san_stress
+$(SANLIB)/tsan/p1hip_host.o: $(CSRC)/p1hip.hip $(HDRS)
+	mkdir -p $(@D)
+	$(HIPCC) -O1 -g -std=c++17 -fPIC --offload-arch=$(ARCH) -fno-omit-frame-pointer -Xarch_host -fsanitize=thread \
+	    -c -o $@ $(CSRC)/p1hip.hip
+$(SANLIB)/tsan/libp1hip.so: $(SANLIB)/tsan/p1hip_host.o $(BUILD)/p1hip_kernels_blob.o
+	$(HIPCC) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+$(SANLIB)/tsan/capi_san_stress: tests/capi_san_stress.cpp include/p1hip.h $(SANLIB)/tsan/libp1hip.so oracle
+	$(SANCXX) $(SANBASE) $(SAN_tsan) -Iinclude -o $@ tests/capi_san_stress.cpp -L$(SANLIB)/tsan -lp1hip \
+	    -Wl,-rpath,'$$ORIGIN' -Loracle -lp1oracle -Wl,-rpath,'$$ORIGIN/../../../oracle'
+
 $(SANDIR)/asan/p1emu: tools/p1emu.cpp $(HDRS)
 	mkdir -p $(@D)
 	$(HIPCC) -O1 -g -std=c++17 -fno-omit-frame-pointer -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
@@ -159,4 +172,4 @@ clean:
 	rm -f p1_amd/libp1hip.so tools/queue_ctl tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios tools/lsp_fake_miner tools/wcal tools/vbank
 	rm -rf $(BUILD)/p1hip_kernels* $(BUILD)/p1hip_host.o
 	$(MAKE) -C oracle clean
-.PHONY: all oracle clean isa variant sanitize sanitize-emu sanitize-lib
+.PHONY: all oracle clean isa variant sanitize sanitize-emu sanitize-lib sanitize-lib-tsan

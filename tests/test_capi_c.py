@@ -104,7 +104,7 @@ def test_host_runtime_under_asan(tmp_path):
     (tests/capi_san_stress.cpp).  Passes only with rc 0 and no report file."""
     env = dict(os.environ,
                ASAN_OPTIONS=f"detect_leaks=1:log_path={tmp_path}/asan",
-               LSAN_OPTIONS=f"suppressions={os.path.join(ROOT, 'tests', 'lsan_rocm.supp')}",
+               LSAN_OPTIONS=f"suppressions={os.path.join(ROOT, 'tests', 'lsan_rocm.supp')}:print_suppressions=0",
                UBSAN_OPTIONS=f"print_stacktrace=1:halt_on_error=1:log_path={tmp_path}/ubsan")
     for k in list(env):
         if k.startswith("P1HIP_"):
