@@ -126,7 +126,10 @@ $(SANDIR)/%/lsp_fake_miner: tests/lsp/lsp_fake_miner.cpp $(HOSTSRC) $(HOSTHDR) o
 # are the shipped code object) and its GPU stress driver; in tools/san, not
 # build/, so that they travel to the GPU box with the tree
 SANLIB := tools/san
-sanitize-lib: $(SANLIB)/libp1hip.so $(SANLIB)/capi_san_stress
+sanitize-lib: $(SANLIB)/libp1hip.so $(SANLIB)/capi_san_stress $(SANLIB)/p1miner
+$(SANLIB)/p1miner: p1_amd/host/p1miner.cpp p1_amd/host/miner_gpu.cpp $(HOSTSRC) $(HOSTHDR) $(SANLIB)/libp1hip.so
+	$(SANCXX) $(SANBASE) $(SAN_asan) -o $@ p1_amd/host/p1miner.cpp p1_amd/host/miner_gpu.cpp $(HOSTSRC) -L$(SANLIB) -lp1hip \
+	    -Wl,-rpath,'$$ORIGIN'
 $(SANLIB)/p1hip_host.o: $(CSRC)/p1hip.hip $(HDRS)
 	mkdir -p $(@D)
 	$(HIPCC) -O1 -g -std=c++17 -fPIC --offload-arch=$(ARCH) -fno-omit-frame-pointer -Xarch_host -fsanitize=address \

@@ -18,7 +18,7 @@ from conftest import ROOT, host_bin
 
 SERVER = host_bin(os.path.join(ROOT, "p1_amd", "p1server"))
 CLIENT = host_bin(os.path.join(ROOT, "p1_amd", "p1client"))
-MINER = os.path.join(ROOT, "p1_amd", "p1miner")
+MINER = host_bin(os.path.join(ROOT, "p1_amd", "p1miner"))
 FAKE = host_bin(os.path.join(ROOT, "tools", "lsp_fake_miner"))
 
 
