@@ -158,6 +158,16 @@ $(SANDIR)/asan/p1emu: tools/p1emu.cpp $(HDRS)
 	$(HIPCC) -O1 -g -std=c++17 -fno-omit-frame-pointer -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
 	    -Xarch_host -fno-sanitize-recover=undefined -DP1_NV2_PLAIN -o $@ tools/p1emu.cpp
 
+# libFuzzer harness of the wire codecs (tests/fuzz/fuzz_codecs.cpp) with
+# ASan + UBSan.  -asan-globals=0: with -fsanitize=fuzzer this clang registers
+# the harness's own string literals twice and ASan stops at start-up with a
+# spurious odr-violation; heap, stack and UB checks are unaffected.
+fuzz: $(SANDIR)/fuzz_codecs
+$(SANDIR)/fuzz_codecs: tests/fuzz/fuzz_codecs.cpp p1_amd/host/bitcoin.cpp p1_amd/host/lsp_message.cpp $(HOSTHDR)
+	mkdir -p $(@D)
+	$(SANCXX) $(SANBASE) -fsanitize=fuzzer,address,undefined -fno-sanitize-recover=undefined -mllvm -asan-globals=0 \
+	    -o $@ tests/fuzz/fuzz_codecs.cpp p1_amd/host/bitcoin.cpp p1_amd/host/lsp_message.cpp
+
 # A/B tuning builds (not used unless P1HIP_LIB points at one):
 #   make variant NAME=x DEVEXTRA='-DP1_FAST_WAVES=5' ISAPOST='--no-e64'
 #   make variant NAME=nv2 DEVEXTRA=-DP1_NV2_PLAIN HOSTEXTRA=-DP1_NV2_PLAIN   (+ P1HIP_NO_SPLIT=1 at run time)
@@ -175,4 +185,4 @@ clean:
 	rm -f p1_amd/libp1hip.so tools/queue_ctl tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios tools/lsp_fake_miner tools/wcal tools/vbank
 	rm -rf $(BUILD)/p1hip_kernels* $(BUILD)/p1hip_host.o
 	$(MAKE) -C oracle clean
-.PHONY: all oracle clean isa variant sanitize sanitize-emu sanitize-lib sanitize-lib-tsan
+.PHONY: all oracle clean isa variant sanitize sanitize-emu sanitize-lib sanitize-lib-tsan fuzz

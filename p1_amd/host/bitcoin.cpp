@@ -13,9 +13,7 @@
 
 namespace bitcoin {
 
-using gojson::ieq;
 using gojson::json_string;
-using gojson::Parser;
 
 Message NewRequest(const std::string& data, uint64_t lower, uint64_t upper) {
   Message m;
@@ -53,56 +51,29 @@ std::string Message::String() const {
 
 std::string Marshal(const Message& m) {
   char buf[160];
-  std::string o = "{\"Type\":" + std::to_string((int)m.Type) + ",\"Data\":";
+  std::string o = "{\"Type\":" + std::to_string(m.Type) + ",\"Data\":";
   json_string(o, m.Data);
   snprintf(buf, sizeof buf, ",\"Lower\":%" PRIu64 ",\"Upper\":%" PRIu64 ",\"Hash\":%" PRIu64 ",\"Nonce\":%" PRIu64 "}",
            m.Lower, m.Upper, m.Hash, m.Nonce);
   return o + buf;
 }
 
-bool Unmarshal(const std::string& json, Message* out) {
-  Parser P{json.data(), json.data() + json.size()};
-  Message m = *out;
-  P.ws();
-  if (P.p >= P.e || *P.p != '{') return false;
-  ++P.p;
-  P.ws();
-  if (P.p < P.e && *P.p == '}') { ++P.p; *out = m; return true; }
-  for (;;) {
-    P.ws();
-    std::string key;
-    if (!P.str(&key)) return false;
-    P.ws();
-    if (P.p >= P.e || *P.p++ != ':') return false;
-    P.ws();
-    if (P.lit("null")) {
-      // Go leaves the field unchanged
-    } else if (ieq(key, "Type")) {
-      uint64_t v;
-      if (!P.u64(&v, true)) return false;
-      m.Type = (MsgType)(int)(int64_t)v;
-    } else if (ieq(key, "Data")) {
-      if (!P.str(&m.Data)) return false;
-    } else if (ieq(key, "Lower")) {
-      if (!P.u64(&m.Lower, false)) return false;
-    } else if (ieq(key, "Upper")) {
-      if (!P.u64(&m.Upper, false)) return false;
-    } else if (ieq(key, "Hash")) {
-      if (!P.u64(&m.Hash, false)) return false;
-    } else if (ieq(key, "Nonce")) {
-      if (!P.u64(&m.Nonce, false)) return false;
-    } else if (!P.skip()) {
-      return false;
-    }
-    P.ws();
-    if (P.p < P.e && *P.p == ',') { ++P.p; continue; }
-    if (P.p < P.e && *P.p == '}') { ++P.p; break; }
-    return false;
-  }
-  P.ws();
-  if (P.p != P.e) return false;
-  *out = m;
-  return true;
+int UnmarshalStatus(const std::string& json, Message* out) {
+  Message m = *out;  // a syntax error leaves *out untouched
+  const gojson::Status st = gojson::decode_struct(json, [&](const std::string& key, const gojson::Value& v) {
+    using gojson::key_matches;
+    if (key_matches(key, "Type")) return gojson::assign_int(v, &m.Type);
+    if (key_matches(key, "Data")) return gojson::assign_string(v, &m.Data);
+    if (key_matches(key, "Lower")) return gojson::assign_uint(v, &m.Lower);
+    if (key_matches(key, "Upper")) return gojson::assign_uint(v, &m.Upper);
+    if (key_matches(key, "Hash")) return gojson::assign_uint(v, &m.Hash);
+    if (key_matches(key, "Nonce")) return gojson::assign_uint(v, &m.Nonce);
+    return gojson::kSet;  // unknown key: skipped
+  });
+  if (st != gojson::kSyntaxError) *out = m;
+  return st;
 }
+
+bool Unmarshal(const std::string& json, Message* out) { return UnmarshalStatus(json, out) == gojson::kOk; }
 
 }  // namespace bitcoin

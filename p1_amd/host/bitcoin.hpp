@@ -25,7 +25,7 @@ namespace bitcoin {
 enum MsgType { Join = 0, Request = 1, Result = 2 };  // message.go:7-13
 
 struct Message {  // message.go:18-23
-  MsgType Type = Join;
+  int64_t Type = Join;  // Go: type MsgType int (64-bit), any value decodes
   std::string Data;
   uint64_t Lower = 0, Upper = 0;
   uint64_t Hash = 0, Nonce = 0;
@@ -42,9 +42,14 @@ uint64_t Hash(const std::string& msg, uint64_t nonce);
 // encoding/json.Marshal of a Message (field order, escaping and number
 // format of Go's encoder).
 std::string Marshal(const Message& m);
-// encoding/json.Unmarshal into a Message; returns false on malformed input
-// (unknown keys are ignored, like Go).
+// encoding/json.Unmarshal into a Message (gojson.hpp: Go 1.4's rules).
+// Returns true when Go's error would be nil.  On a type error (e.g. a
+// negative Lower) *out holds Go's partial decode and false is returned; on
+// a syntax error *out is untouched.  miner.go:55 and client.go:53 ignore the
+// error and use whatever was decoded.
 bool Unmarshal(const std::string& json, Message* out);
+// The same, returning gojson::Status (0 ok, 1 type error, 2 syntax error).
+int UnmarshalStatus(const std::string& json, Message* out);
 
 struct HipError : std::runtime_error {
   int rc;

@@ -108,53 +108,65 @@ std::string Marshal(const Message& m) {
   return o + "}";
 }
 
-bool Unmarshal(const std::string& json, Message* out) {
-  gojson::Parser P{json.data(), json.data() + json.size()};
-  Message m = *out;
-  P.ws();
-  if (P.p >= P.e || *P.p != '{') return false;
-  ++P.p;
-  P.ws();
-  if (P.p < P.e && *P.p == '}') {
-    ++P.p;
-  } else {
-    for (;;) {
-      P.ws();
-      std::string key;
-      if (!P.str(&key)) return false;
-      P.ws();
-      if (P.p >= P.e || *P.p++ != ':') return false;
-      P.ws();
-      if (P.lit("null")) {
-        if (gojson::ieq(key, "Payload")) {  // null into a slice sets it to nil
-          m.Payload.clear();
-          m.PayloadNil = true;
-        }
-      } else if (gojson::ieq(key, "Type")) {
-        if (!P.i64(&m.Type)) return false;
-      } else if (gojson::ieq(key, "ConnID")) {
-        if (!P.i64(&m.ConnID)) return false;
-      } else if (gojson::ieq(key, "SeqNum")) {
-        if (!P.i64(&m.SeqNum)) return false;
-      } else if (gojson::ieq(key, "Size")) {
-        if (!P.i64(&m.Size)) return false;
-      } else if (gojson::ieq(key, "Payload")) {
-        std::string b64;
-        if (!P.str(&b64) || !Base64Decode(b64, &m.Payload)) return false;
-        m.PayloadNil = false;
-      } else if (!P.skip()) {
-        return false;
-      }
-      P.ws();
-      if (P.p < P.e && *P.p == ',') { ++P.p; continue; }
-      if (P.p < P.e && *P.p == '}') { ++P.p; break; }
-      return false;
-    }
+// Go's d.array into a []byte: each element decoded as a uint8 (a failed
+// element keeps the byte already at that index), the length set to the
+// element count, never nil
+static gojson::Assign assign_byte_array(const gojson::Value& v, Message* m) {
+  gojson::Reader R{v.b + 1, v.e};
+  gojson::Assign st = gojson::kSet;
+  size_t i = 0;
+  for (;;) {
+    R.ws();
+    if (*R.p == ']') break;
+    const gojson::Value x = R.value();
+    if (i >= m->Payload.size()) m->Payload.push_back(0);
+    uint64_t b = 0;
+    if (x.kind == gojson::kNumber && gojson::parse_uint(x, &b) && b <= 255) m->Payload[i] = (uint8_t)b;
+    else if (x.kind == gojson::kNumber) st = gojson::kSkip;  // ParseUint / OverflowUint
+    else if (x.kind != gojson::kNull) st = gojson::kSkip;   // string / bool / array / object into uint8
+    ++i;
+    R.ws();
+    if (*R.p == ',') ++R.p;
   }
-  P.ws();
-  if (P.p != P.e) return false;
-  *out = m;
-  return true;
+  m->Payload.resize(i);
+  m->PayloadNil = false;
+  return st;
 }
+
+static gojson::Assign assign_payload(const gojson::Value& v, Message* m) {
+  switch (v.kind) {
+    case gojson::kNull:  // null into a slice sets it to nil
+      m->Payload.clear();
+      m->PayloadNil = true;
+      return gojson::kSet;
+    case gojson::kString: {
+      std::vector<uint8_t> b;
+      if (!Base64Decode(gojson::unquote(v), &b)) return gojson::kSkip;
+      m->Payload = std::move(b);
+      m->PayloadNil = false;
+      return gojson::kSet;
+    }
+    case gojson::kArray: return assign_byte_array(v, m);
+    case gojson::kNumber: return gojson::kAbort;
+    default: return gojson::kSkip;
+  }
+}
+
+int UnmarshalStatus(const std::string& json, Message* out) {
+  Message m = *out;  // a syntax error leaves *out untouched
+  const gojson::Status st = gojson::decode_struct(json, [&](const std::string& key, const gojson::Value& v) {
+    using gojson::key_matches;
+    if (key_matches(key, "Type")) return gojson::assign_int(v, &m.Type);
+    if (key_matches(key, "ConnID")) return gojson::assign_int(v, &m.ConnID);
+    if (key_matches(key, "SeqNum")) return gojson::assign_int(v, &m.SeqNum);
+    if (key_matches(key, "Size")) return gojson::assign_int(v, &m.Size);
+    if (key_matches(key, "Payload")) return assign_payload(v, &m);
+    return gojson::kSet;  // unknown key: skipped
+  });
+  if (st != gojson::kSyntaxError) *out = m;
+  return st;
+}
+
+bool Unmarshal(const std::string& json, Message* out) { return UnmarshalStatus(json, out) == gojson::kOk; }
 
 }  // namespace lsp

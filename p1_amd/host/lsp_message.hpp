@@ -34,8 +34,12 @@ Message NewData(int64_t connID, int64_t seqNum, int64_t size, const std::string&
 Message NewAck(int64_t connID, int64_t seqNum);                                          // message.go:43-49
 
 std::string Marshal(const Message& m);
-// false on malformed JSON or a Payload that is not valid padded base64
+// encoding/json.Unmarshal (gojson.hpp: Go 1.4's rules): true when Go's error
+// would be nil; on a type error (e.g. a Payload that is not padded base64)
+// *out holds the partial decode, on a syntax error it is untouched.  The LSP
+// endpoints drop every datagram that is not error-free (lsp.cpp).
 bool Unmarshal(const std::string& json, Message* out);
+int UnmarshalStatus(const std::string& json, Message* out);  // gojson::Status
 
 std::string Base64Encode(const std::vector<uint8_t>& b);
 bool Base64Decode(const std::string& s, std::vector<uint8_t>* out);

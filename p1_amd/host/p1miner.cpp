@@ -18,9 +18,11 @@
 //                                        one JSON Message per stdin line; every
 //                                        line is answered with one JSON Result
 //                                        line (miner.go:49-67 scans whatever it
-//                                        decoded; a bad line scans [0, 0] of "")
+//                                        decoded, as Go's Unmarshal leaves it)
 //   p1miner json                         re-marshals stdin JSON lines (no GPU;
-//                                        wire-format tests)
+//                                        wire-format tests): "ERROR" for a
+//                                        syntax error, "TYPEERROR\t" before
+//                                        Go's partial decode on a type error
 //   p1miner lsp-json                     re-marshals stdin lsp.Message JSON lines
 //                                        (lsp/message.go; no GPU)
 //   p1miner lsp-wrap <connID> <seq>      each stdin bitcoin.Message JSON line ->
@@ -40,6 +42,7 @@
 
 #include "../../include/p1hip.h"
 #include "bitcoin.hpp"
+#include "gojson.hpp"
 #include "lsp.hpp"
 #include "lsp_message.hpp"
 #include "lspnet.hpp"
@@ -96,7 +99,7 @@ static int run_lsp(int argc, char** argv) {
     std::string buf;
     if (!cli->Read(&buf)) break;
     bitcoin::Message req;
-    if (!bitcoin::Unmarshal(buf, &req)) req = bitcoin::Message();  // miner.go:54-55 ignores the error
+    bitcoin::Unmarshal(buf, &req);  // miner.go:54-55: a fresh Message, the error ignored (partial decode kept)
     const bitcoin::Message res = miner::HandleRequest(req, chunk);
     if (!cli->Write(bitcoin::Marshal(res))) break;
   }
@@ -128,8 +131,11 @@ int main(int argc, char** argv) {
       std::string line;
       while (std::getline(std::cin, line)) {
         bitcoin::Message m;
-        if (!bitcoin::Unmarshal(line, &m)) { printf("ERROR\n"); continue; }
-        printf("%s\t%s\n", bitcoin::Marshal(m).c_str(), m.String().c_str());
+        const int st = bitcoin::UnmarshalStatus(line, &m);
+        if (st == gojson::kSyntaxError) { printf("ERROR\n"); continue; }
+        // fwrite, not %s: a decoded string may hold NUL bytes
+        const std::string o = (st == gojson::kTypeError ? "TYPEERROR\t" : "") + bitcoin::Marshal(m) + "\t" + m.String() + "\n";
+        fwrite(o.data(), 1, o.size(), stdout);
       }
       return 0;
     }
@@ -137,8 +143,11 @@ int main(int argc, char** argv) {
       std::string line;
       while (std::getline(std::cin, line)) {
         lsp::Message m;
-        if (!lsp::Unmarshal(line, &m)) { printf("ERROR\n"); continue; }
-        printf("%s\t%s\n", lsp::Marshal(m).c_str(), m.String().c_str());
+        const int st = lsp::UnmarshalStatus(line, &m);
+        if (st == gojson::kSyntaxError) { printf("ERROR\n"); continue; }
+        // fwrite, not %s: a decoded string may hold NUL bytes
+        const std::string o = (st == gojson::kTypeError ? "TYPEERROR\t" : "") + lsp::Marshal(m) + "\t" + m.String() + "\n";
+        fwrite(o.data(), 1, o.size(), stdout);
       }
       return 0;
     }
@@ -183,12 +192,13 @@ int main(int argc, char** argv) {
       if (rc != P1HIP_OK) { fprintf(stderr, "p1hip init: %s\n", p1hip_last_error()); return 1; }
       std::string line;
       while (std::getline(std::cin, line)) {
-        // miner.go:54-55 decodes into a zero Message and ignores the error, then
-        // scans [Lower, Upper] whatever the Type: an undecodable line is the
-        // one-nonce request ("", [0, 0]) and is answered like any other, so a
+        // miner.go:54-55 decodes into a fresh Message and ignores the error,
+        // then scans [Lower, Upper] whatever the Type: a line with a type
+        // error scans what Go's partial decode holds, a line that is not JSON
+        // the one-nonce request ("", [0, 0]); every line is answered, so a
         // server never waits on a miner that stays silent.
         bitcoin::Message req;
-        if (!bitcoin::Unmarshal(line, &req)) req = bitcoin::Message();
+        bitcoin::Unmarshal(line, &req);
         bitcoin::Message res = miner::HandleRequest(req, chunk);
         printf("%s\n", bitcoin::Marshal(res).c_str());
         fflush(stdout);

@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "bitcoin.hpp"
+#include "gojson.hpp"
 #include "lsp.hpp"
 #include "lspnet.hpp"
 #include "scheduler.hpp"
@@ -69,8 +70,12 @@ int run_lsp(int port, const lsp::Params& prm, uint64_t chunk, long exit_after) {
       if (S.IsMiner(id)) S.LoseMiner(id);
       else S.CancelClient(id);
     } else {
+      // server.go:117 ignores Unmarshal's error and switches on whatever was
+      // decoded: a type error (say a negative Lower) still yields the rest of
+      // the message.  Unlike the reference, a payload that is not JSON at all
+      // is dropped rather than read as a zero Message (a Join).
       bitcoin::Message m;
-      if (bitcoin::Unmarshal(payload, &m)) {
+      if (bitcoin::UnmarshalStatus(payload, &m) != gojson::kSyntaxError) {
         switch (m.Type) {
           case bitcoin::Join: S.AddMiner(id); break;
           case bitcoin::Request: S.Submit(id, m.Data, m.Lower, m.Upper); break;
@@ -312,7 +317,7 @@ int main(int argc, char** argv) {
     std::string line;
     while (std::getline(std::cin, line)) {
       bitcoin::Message req;
-      if (!bitcoin::Unmarshal(line, &req) || req.Type != bitcoin::Request) continue;
+      if (bitcoin::UnmarshalStatus(line, &req) == gojson::kSyntaxError || req.Type != bitcoin::Request) continue;
       srv.submit(req.Data, req.Lower, req.Upper);
     }
     // stdio has no per-client connection (the reference answers each client

@@ -51,7 +51,7 @@ int main(int argc, char** argv) {
     if (!cli->Read(&buf)) break;
     if (answered == die_after) _exit(3);  // vanish: no answer, no Close
     bitcoin::Message req;
-    if (!bitcoin::Unmarshal(buf, &req)) req = bitcoin::Message();
+    bitcoin::Unmarshal(buf, &req);  // miner.go:54-55: the error is ignored
     if (logp && *logp) {
       if (FILE* f = fopen(logp, "a")) {
         fprintf(f, "%llu %llu\n", (unsigned long long)req.Lower, (unsigned long long)req.Upper);
