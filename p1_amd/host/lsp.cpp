@@ -468,6 +468,12 @@ class ServerImpl : public Server {
     auto it = conns_.find(m.ConnID);
     if (it == conns_.end()) return;
     Conn& c = it->second;
+    // Only the connection's own address speaks for it.  The reference looks
+    // the connection up by ConnID alone (server_impl.go:198-204), so any
+    // datagram naming a live id and a plausible SeqNum could inject a
+    // message or ack one the client never had delivered; a correct client
+    // always sends from the socket it connected with.
+    if (!(c.p.addr == from)) return;
     if (m.Type == MsgData && !size_ok(m)) return;
     c.p.idle = 0;
     const SendFn send = sender(c);

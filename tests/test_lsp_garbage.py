@@ -1,0 +1,171 @@
+"""The bitcoin system over LSP while other sockets throw garbage at the
+server (CPU; ASan + UBSan builds from `make sanitize`).
+
+Beside a working system (p1server lsp, 2 test-double miners, 3 clients)
+four sockets send ~24,000 datagrams at the server's port: random bytes,
+random JSON fragments, well-formed LSP messages with random Type / ConnID /
+SeqNum / Size / Payload (some naming the live connections' ids), mutated
+valid datagrams, 2-60 KB datagrams, and -- on connections of their own --
+Data whose payload is garbage, a broken bitcoin message, a small Request or
+a stray Result.  The clients must still print the exact answers, the server
+must still be running, and no sanitizer may report.  The garbage sockets
+never send a Join: a miner that joins and answers with wrong hashes is
+trusted by the protocol (the reference's too) and is no test of robustness.
+"""
+import base64
+import json
+import os
+import random
+import socket
+import subprocess
+import threading
+import time
+
+import pytest
+
+from conftest import ROOT
+
+SAN = os.path.join(ROOT, "build", "san", "asan")
+SANCXX = "/opt/rocm/lib/llvm/bin/clang++"
+
+pytestmark = pytest.mark.skipif(not os.path.exists(SANCXX), reason="ROCm clang (sanitizer runtimes) not present")
+
+ATOMS = [b'{', b'}', b'[', b']', b',', b':', b'"', b'"Type"', b'"ConnID"', b'"SeqNum"', b'"Payload"', b'1', b'-1',
+         b'null', b'true', b'"aGk="', b'0', b'99999999999999999999', b'\xff', b'\\u0000']
+
+
+def lsp_msg(t, c, s, size, payload):
+    return json.dumps({"Type": t, "ConnID": c, "SeqNum": s, "Size": size, "Payload": payload}).encode()
+
+
+def b64(b):
+    return base64.b64encode(b).decode()
+
+
+def bitcoin_garbage(rnd):
+    k = rnd.randrange(6)
+    if k == 0:
+        return bytes(rnd.randrange(256) for _ in range(rnd.randrange(60)))
+    if k == 1:
+        return b'{"Type":1,"Data":"x","Lower":'  # truncated
+    if k == 2:  # a small request (answered to a connection that never acks)
+        lo = rnd.randrange(10**6)
+        return json.dumps({"Type": 1, "Data": "g", "Lower": lo, "Upper": lo + rnd.randrange(300)}).encode()
+    if k == 3:  # a result from a connection that is no miner
+        return json.dumps({"Type": 2, "Hash": rnd.randrange(2**64), "Nonce": rnd.randrange(2**64)}).encode()
+    if k == 4:  # type errors
+        return b'{"Type":1,"Data":"g","Lower":-4,"Upper":"9"}'
+    return json.dumps({"Type": rnd.choice([-1, 3, 2**40]), "Data": "é"}).encode()
+
+
+def datagram(rnd, seq_hint):
+    k = rnd.randrange(6)
+    if k == 0:
+        return bytes(rnd.randrange(256) for _ in range(rnd.randrange(1, 200)))
+    if k == 1:
+        return b"".join(rnd.choice(ATOMS) for _ in range(rnd.randrange(1, 15)))
+    if k == 2:
+        payload = rnd.choice([None, "", "!!!", b64(bitcoin_garbage(rnd)), b64(os.urandom(rnd.randrange(40)))])
+        return lsp_msg(rnd.choice([0, 1, 2, 3, -1]), rnd.choice([0, 1, 2, 3, 4, 5, 6, 7, 99, -1, 2**62]),
+                       rnd.choice([0, 1, seq_hint, seq_hint + 1, -5, 2**40, 2**63 - 1]),
+                       rnd.choice([0, 1, 5, -3, 2**31, 2**62]), payload)
+    if k == 3:
+        m = bytearray(lsp_msg(1, rnd.randrange(1, 8), rnd.randrange(1, 30), 5, "aGVsbG8="))
+        for _ in range(rnd.randrange(1, 4)):
+            m[rnd.randrange(len(m))] = rnd.randrange(256)
+        return bytes(m)
+    if k == 4:
+        return b"[" * rnd.randrange(2000, 60000)
+    return lsp_msg(1, rnd.randrange(1, 8), rnd.randrange(1, 40), 0, b64(b"x" * rnd.randrange(1500, 2500)))
+
+
+def own_connection(sock, addr, rnd, stop):
+    """Connect, then Data on our own connection (garbage bitcoin payloads)."""
+    sock.sendto(lsp_msg(0, 0, 0, 0, None), addr)
+    sock.settimeout(1.0)
+    try:
+        ack = json.loads(sock.recv(4096))
+        conn = ack["ConnID"]
+    except (OSError, ValueError, KeyError):
+        return
+    seq = 1
+    while not stop.is_set() and seq < 400:
+        p = bitcoin_garbage(rnd)
+        sock.sendto(lsp_msg(1, conn, seq, len(p), b64(p)), addr)
+        seq += 1
+        time.sleep(0.002)
+
+
+def spray(port, seed, count, stop):
+    rnd = random.Random(seed)
+    addr = ("127.0.0.1", port)
+    with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+        if seed % 2:
+            own_connection(s, addr, rnd, stop)
+        s.setblocking(False)
+        for i in range(count):
+            if stop.is_set():
+                break
+            try:
+                s.sendto(datagram(rnd, i % 40), addr)
+            except OSError:
+                pass  # e.g. EMSGSIZE, ECONNREFUSED from an earlier send
+            try:
+                while True:
+                    s.recv(65536)  # drain what the server sends back
+            except OSError:
+                pass
+            if i % 200 == 0:
+                time.sleep(0.01)
+
+
+def test_system_survives_garbage_datagrams(tmp_path, oracle_mod):
+    subprocess.run(["make", "-s", "-j8", "-C", ROOT, "sanitize"], check=True, stdout=subprocess.DEVNULL)
+    env = dict(os.environ,
+               ASAN_OPTIONS=f"detect_leaks=1:log_path={tmp_path}/asan",
+               UBSAN_OPTIONS=f"print_stacktrace=1:halt_on_error=1:log_path={tmp_path}/ubsan")
+    prm = ["--epoch-millis", "100", "--epoch-limit", "20", "--window", "4"]
+    procs = []
+    stop = threading.Event()
+    try:
+        srv = subprocess.Popen([os.path.join(SAN, "p1server"), "--chunk", "1500"] + prm + ["lsp", "0"],
+                               stdout=subprocess.PIPE, text=True, env=env)
+        procs.append(srv)
+        line = srv.stdout.readline()
+        assert line.startswith("Server listening on port"), line
+        port = int(line.split()[-1])
+        hp = f"127.0.0.1:{port}"
+        for _ in range(2):
+            procs.append(subprocess.Popen([os.path.join(SAN, "lsp_fake_miner"), hp] + prm, env=env,
+                                          stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
+        sprayers = [threading.Thread(target=spray, args=(port, seed, 6000, stop)) for seed in range(4)]
+        for t in sprayers:
+            t.start()
+        jobs = [("bradfitz", 9999), ("cmu440", 14999), ("x" * 60, 7000)]
+        clients = [subprocess.Popen([os.path.join(SAN, "p1client"), hp, m, str(mx)] + prm, stdout=subprocess.PIPE,
+                                    stderr=subprocess.PIPE, text=True, env=env) for m, mx in jobs]
+        for (m, mx), c in zip(jobs, clients):
+            out, err = c.communicate(timeout=240)
+            h, n = oracle_mod.scan(m, 0, mx, threads=4)
+            assert out.strip() == f"Result {h} {n}", (m, out, err[-2000:])
+        stop.set()
+        for t in sprayers:
+            t.join(timeout=60)
+        assert srv.poll() is None, "the server exited"
+        # still serving after the storm
+        c = subprocess.run([os.path.join(SAN, "p1client"), hp, "bradfitz", "9999"] + prm, capture_output=True,
+                           text=True, timeout=120, env=env)
+        assert c.stdout.strip() == "Result 1419516646206828 9898", c.stdout + c.stderr[-2000:]
+    finally:
+        stop.set()
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    reports = sorted(f for f in os.listdir(tmp_path) if f.split(".")[0] in ("asan", "ubsan"))
+    assert not reports, "".join(open(os.path.join(tmp_path, f)).read()[:4000] for f in reports)
