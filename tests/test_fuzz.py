@@ -2,7 +2,7 @@
 coverage-guided fuzzer and against an independent JSON grammar.
 
 - `make fuzz` builds tests/fuzz/fuzz_codecs.cpp with libFuzzer + ASan +
-  UBSan; here it runs for 20 s from the seeds in tests/fuzz/seeds (a longer
+  UBSan; here it runs for 10 s from the seeds in tests/fuzz/seeds (a longer
   run: tools/fuzz.sh).  Properties: no sanitizer report; a syntax error
   leaves the message untouched; any other input re-encodes to an error-free
   fixed point; base64 decode(encode(decode(s))) == decode(s).
@@ -26,11 +26,11 @@ SANCXX = "/opt/rocm/lib/llvm/bin/clang++"
 
 
 @pytest.mark.skipif(not os.path.exists(SANCXX), reason="ROCm clang (libFuzzer runtime) not present")
-def test_codec_fuzzer_20s(tmp_path):
+def test_codec_fuzzer_10s(tmp_path):
     subprocess.run(["make", "-s", "-C", ROOT, "fuzz"], check=True, stdout=subprocess.DEVNULL)
     corpus = tmp_path / "corpus"
     shutil.copytree(os.path.join(ROOT, "tests", "fuzz", "seeds"), corpus)
-    r = subprocess.run([FUZZ, "-max_total_time=20", "-print_final_stats=1", "-max_len=4096", str(corpus)],
+    r = subprocess.run([FUZZ, "-max_total_time=10", "-print_final_stats=1", "-max_len=4096", str(corpus)],
                        capture_output=True, text=True, timeout=120, cwd=tmp_path)
     assert r.returncode == 0, r.stderr[-4000:]
     runs = [ln for ln in r.stderr.splitlines() if ln.startswith("stat::number_of_executed_units")]
