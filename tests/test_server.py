@@ -77,6 +77,27 @@ def test_scheduler_unit(tmp_path):
     assert r.stdout.strip() == "sched_test: ok"
 
 
+def test_scheduler_randomized_simulation(tmp_path):
+    """scheduler.hpp against a brute-force model under random joins, losses
+    (holding a chunk, or after computing it), departed clients, stray
+    Results, results out of order, empty ranges and ranges at the u64 top
+    (tests/sched_sim.cpp), built with ASan + UBSan.  A stand-in hash with a
+    message-dependent range makes equal minima common, so the lowest-nonce
+    rule is exercised within and across chunks (dropping the requeue of a
+    lost chunk, reversing the tie rule or widening a chunk by one nonce each
+    fail it)."""
+    exe = str(tmp_path / "sched_sim")
+    subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=undefined", "-o", exe, os.path.join(ROOT, "tests", "sched_sim.cpp")],
+                   check=True)
+    total = 0
+    for seed in range(1, 25):
+        r = subprocess.run([exe, str(seed), "3000"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and r.stdout.startswith("sched_sim: ok"), (seed, r.stdout, r.stderr[-2000:])
+        total += int(r.stdout.split()[2])
+    assert total > 24 * 200  # requests completed and checked
+
+
 def test_usage():
     assert server([]).returncode == 2
     assert server(["--chunk", "0", "scan", "a", "0", "1"]).returncode == 2
