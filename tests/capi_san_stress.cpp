@@ -35,6 +35,14 @@
 
 #include "p1hip.h"
 
+#if defined(__has_feature)
+#if __has_feature(address_sanitizer)
+#include <sanitizer/lsan_interface.h>
+#include <unistd.h>
+#define P1_ASAN_BUILD 1
+#endif
+#endif
+
 extern "C" {
 uint64_t p1o_hash(const uint8_t* msg, size_t len, uint64_t nonce);
 int p1o_scan_mt(const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, int nthreads, uint64_t* out_hash,
@@ -174,8 +182,13 @@ bool phase_scan(std::mt19937_64& g, double secs, int oracle_threads, const char*
                 uint64_t big = 200000000) {
   const auto end = Clock::now() + std::chrono::duration<double>(secs);
   long cases = 0, nonces = 0;
+  auto beat = Clock::now() + std::chrono::seconds(20);
   // exact-checkable sizes most of the time, larger fast-path ranges sometimes
   while (Clock::now() < end && !g_fail) {
+    if (Clock::now() > beat) {  // a long run keeps writing (a silent run looks hung)
+      printf("%s ... %ld scans\n", tag, cases);
+      beat += std::chrono::seconds(20);
+    }
     const std::string m = rand_msg(g);
     const int sz = std::uniform_int_distribution<int>(0, 9)(g);
     uint64_t span = sz < 3 ? std::uniform_int_distribution<uint64_t>(1, 70000)(g)
@@ -284,6 +297,7 @@ bool phase_reinit(std::mt19937_64& g) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  setvbuf(stdout, nullptr, _IOLBF, 0);  // progress lines reach a log file at once
   const double secs = argc > 1 ? atof(argv[1]) : 30.0;
   const uint64_t seed = argc > 2 ? strtoull(argv[2], nullptr, 10) : 440;
   std::mt19937_64 g(seed);
@@ -303,5 +317,14 @@ int main(int argc, char** argv) {
             phase_reduce(g) && phase_knobs(g, secs * 0.3) && phase_reinit(g);
   p1hip_shutdown();
   printf(ok ? "ok\n" : "FAILED\n");
+#ifdef P1_ASAN_BUILD
+  // Leak-check now, then leave without the ROCm runtime's static
+  // destructors: under ROCm's ASan runtime their frees at exit can trip an
+  // allocator CHECK ("!dev_runtime_unloaded_", sanitizer_allocator_device.h)
+  // inside libhsa-runtime64, after every phase has passed (r04p).
+  fflush(stdout);
+  __lsan_do_leak_check();
+  _exit(ok ? 0 : 1);
+#endif
   return ok ? 0 : 1;
 }
