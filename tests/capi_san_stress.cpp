@@ -15,6 +15,8 @@
 //           oracle up to 3e5 nonces, above that by re-hash + split-min
 //   threads 4 host threads calling p1hip_scan / p1hip_hash at once
 //   reduce  p1hip_reduce_pairs on crafted arrays (ties, all-UINT64_MAX, n = 0)
+//   chaos   4 scanning threads beside a 5th that shuts down / re-opens the
+//           library and reads its stats, identity and knobs
 //   knobs   P1HIP_TEST_KNOBS paths: 3 logical devices with host combine,
 //           multi-launch, MODE 5 table refused (re-plan), small share spans,
 //           an injected device failure (rc -2) and recovery
@@ -244,6 +246,56 @@ bool phase_reduce(std::mt19937_64& g) {
   return true;
 }
 
+// scans on 4 threads while a 5th shuts the library down, re-opens it and
+// reads its stats and identity: every scan must still succeed (a scan after
+// a shutdown re-initialises lazily) with the exact answer
+bool phase_chaos(uint64_t seed, double secs) {
+  std::atomic<bool> stop{false};
+  std::atomic<int> bad{0};
+  std::atomic<long> cycles{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 4; ++t)
+    ts.emplace_back([&, t] {
+      std::mt19937_64 g(seed + 2000 + t);
+      long n = 0;
+      while (!stop && !bad) {
+        const std::string m = rand_msg(g);
+        uint64_t lo, hi;
+        rand_range(g, std::uniform_int_distribution<uint64_t>(1, 200000)(g), &lo, &hi);
+        if (!check_scan(m, lo, hi, 2)) bad = 1;
+        ++n;
+      }
+      printf("chaos thread %d: %ld scans\n", t, n);
+    });
+  ts.emplace_back([&] {
+    std::mt19937_64 g(seed + 3000);
+    const int one[1] = {0};
+    while (!stop && !bad) {
+      switch (g() % 8) {
+        case 0: p1hip_shutdown(); break;
+        case 1: if (p1hip_init(1, nullptr) != P1HIP_OK) bad = 2; break;
+        case 2: if (p1hip_init_devices(one, 1) != P1HIP_OK) bad = 3; break;
+        case 3: { p1hip_stats_t st; if (p1hip_get_stats(&st) != P1HIP_OK) bad = 4; break; }
+        case 4: p1hip_reset_stats(); break;
+        case 5: { p1hip_device_info_t in; (void)p1hip_device_info(0, &in); break; }  // may be closed: rc varies
+        case 6: p1hip_set_profiling((int)(g() & 1)); break;
+        default: if (strlen(p1hip_test_knobs()) != 0) bad = 5; break;
+      }
+      ++cycles;
+      std::this_thread::sleep_for(std::chrono::milliseconds(g() % 20));
+    }
+  });
+  std::this_thread::sleep_for(std::chrono::duration<double>(secs));
+  stop = true;
+  for (auto& t : ts) t.join();
+  CHECK(!bad, "chaos: failure %d", bad.load());
+  // leave the library open on one device for the phases that follow
+  p1hip_shutdown();
+  CHECK(p1hip_init(1, nullptr) == P1HIP_OK, "chaos: re-init");
+  printf("chaos ok: %ld lifecycle calls beside the scans\n", cycles.load());
+  return true;
+}
+
 void set_knobs(const std::vector<std::pair<const char*, const char*>>& kv) {
   setenv("P1HIP_TEST_KNOBS", "1", 1);
   for (auto& p : kv) setenv(p.first, p.second, 1);
@@ -313,8 +365,8 @@ int main(int argc, char** argv) {
     fprintf(stderr, "init rc %d: %s\n", rc, p1hip_last_error());
     return 1;
   }
-  bool ok = phase_args() && phase_scan(g, secs * 0.3, 8, "scan") && phase_threads(seed, secs * 0.2) &&
-            phase_reduce(g) && phase_knobs(g, secs * 0.3) && phase_reinit(g);
+  bool ok = phase_args() && phase_scan(g, secs * 0.25, 8, "scan") && phase_threads(seed, secs * 0.2) &&
+            phase_reduce(g) && phase_chaos(seed, secs * 0.1) && phase_knobs(g, secs * 0.25) && phase_reinit(g);
   p1hip_shutdown();
   printf(ok ? "ok\n" : "FAILED\n");
 #ifdef P1_ASAN_BUILD
