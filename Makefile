@@ -162,7 +162,13 @@ $(SANDIR)/asan/p1emu: tools/p1emu.cpp $(HDRS)
 # ASan + UBSan.  -asan-globals=0: with -fsanitize=fuzzer this clang registers
 # the harness's own string literals twice and ASan stops at start-up with a
 # spurious odr-violation; heap, stack and UB checks are unaffected.
-fuzz: $(SANDIR)/fuzz_codecs
+fuzz: $(SANDIR)/fuzz_codecs $(SANDIR)/fuzz_planner
+# the host-side planner (make_plan, plan_shards); hipcc for the HIP headers,
+# sanitizers and libFuzzer on the host side only
+$(SANDIR)/fuzz_planner: tests/fuzz/fuzz_planner.cpp $(HDRS)
+	mkdir -p $(@D)
+	$(HIPCC) -O1 -g -std=c++17 -Xarch_host -fsanitize=fuzzer -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+	    -Xarch_host -fno-sanitize-recover=undefined -o $@ tests/fuzz/fuzz_planner.cpp
 $(SANDIR)/fuzz_codecs: tests/fuzz/fuzz_codecs.cpp p1_amd/host/bitcoin.cpp p1_amd/host/lsp_message.cpp $(HOSTHDR)
 	mkdir -p $(@D)
 	$(SANCXX) $(SANBASE) -fsanitize=fuzzer,address,undefined -fno-sanitize-recover=undefined -mllvm -asan-globals=0 \

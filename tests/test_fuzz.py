@@ -37,6 +37,20 @@ def test_codec_fuzzer_10s(tmp_path):
     assert runs and int(runs[0].split()[-1]) > 10000, r.stderr[-2000:]
 
 
+@pytest.mark.skipif(not os.path.exists(SANCXX), reason="ROCm clang (libFuzzer runtime) not present")
+def test_planner_fuzzer_10s(tmp_path):
+    """planner.hpp (make_plan, plan_shards) on fuzzer-chosen lengths, ranges
+    near decade edges and the u64 top, shard counts and planner switches
+    (tests/fuzz/fuzz_planner.cpp): every plan succeeds and hashes exactly
+    upper-lower+1 nonces; shards are in order, contiguous and cover the range."""
+    subprocess.run(["make", "-s", "-C", ROOT, "fuzz"], check=True, stdout=subprocess.DEVNULL)
+    r = subprocess.run([os.path.join(ROOT, "build", "san", "fuzz_planner"), "-max_total_time=10", "-seed=440",
+                        "-print_final_stats=1"], capture_output=True, text=True, timeout=120, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-4000:]
+    runs = [ln for ln in r.stderr.splitlines() if ln.startswith("stat::number_of_executed_units")]
+    assert runs and int(runs[0].split()[-1]) > 2000, r.stderr[-2000:]
+
+
 ATOMS = ['{', '}', '[', ']', ',', ':', '"', '"a"', '"Type"', '"Data"', '"Lower"', '1', '0', '-', '01', '1.5', '1.',
          '1e5', '1E+2', '-0', 'true', 'false', 'null', 'nul', ' ', '\t', '\n', '\\', '\\u00e9', '\\ud800', '\\x',
          'é', ' ', '\x01', "'", '"\\"', '"\\\\"', '"\\/"', '"\\u12"', '2e', '.5']
