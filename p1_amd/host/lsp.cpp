@@ -58,6 +58,7 @@ struct Peer {
   std::deque<Out> out;    // seq base .. next_seq-1
   int64_t expect = 1;     // next sequence number to deliver in order
   std::map<int64_t, std::string> early;  // received ahead of `expect`
+  size_t early_bytes = 0;                 // payload bytes held in `early`
   bool got_data = false;  // any data message received (heartbeat choice)
   int idle = 0;           // epochs since anything arrived from the peer
   bool lost = false;
@@ -109,21 +110,29 @@ void on_ack(Peer& p, int64_t seq, int window, const SendFn& send) {
 // and never our own window: anything kMaxEarly or more ahead is dropped
 // un-acked, as if lost (the sender resends it an epoch later), which bounds
 // `early` instead of letting a faulty peer grow it without limit.
+// The same holds for bytes: a correct sender's early messages are at most a
+// window of them, so more than kMaxEarlyBytes of payload held ahead of
+// `expect` is a faulty peer, and a new early message beyond it is dropped
+// un-acked too (64 KB datagrams x 2^16 sequence numbers would be 4 GB).
 constexpr int64_t kMaxEarly = 1 << 16;
+constexpr size_t kMaxEarlyBytes = 64u << 20;
 void on_data(Peer& p, Message& m, int window, const SendFn& send, const DeliverFn& deliver) {
   (void)window;
   if (m.SeqNum >= p.expect + kMaxEarly) return;
+  if (m.SeqNum > p.expect && !p.early.count(m.SeqNum) && p.early_bytes + m.Payload.size() > kMaxEarlyBytes) return;
   send(NewAck(p.conn_id, m.SeqNum));
   p.got_data = true;
   if (m.SeqNum < p.expect) return;
   std::string payload(m.Payload.begin(), m.Payload.end());
   if (m.SeqNum > p.expect) {
-    p.early.emplace(m.SeqNum, std::move(payload));
+    const size_t n = payload.size();
+    if (p.early.emplace(m.SeqNum, std::move(payload)).second) p.early_bytes += n;
     return;
   }
   deliver(std::move(payload));
   p.expect++;
   for (auto it = p.early.find(p.expect); it != p.early.end(); it = p.early.find(p.expect)) {
+    p.early_bytes -= it->second.size();
     deliver(std::move(it->second));
     p.early.erase(it);
     p.expect++;

@@ -169,3 +169,67 @@ def test_system_survives_garbage_datagrams(tmp_path, oracle_mod):
                 p.wait()
     reports = sorted(f for f in os.listdir(tmp_path) if f.split(".")[0] in ("asan", "ubsan"))
     assert not reports, "".join(open(os.path.join(tmp_path, f)).read()[:4000] for f in reports)
+
+
+def rss_kb(pid):
+    with open(f"/proc/{pid}/status") as f:
+        for line in f:
+            if line.startswith("VmRSS:"):
+                return int(line.split()[1])
+    return 0
+
+
+def test_early_buffer_is_bounded_in_bytes():
+    """A connected peer that sends only messages ahead of the next expected
+    sequence number (never the one the receiver waits for) makes the server
+    hold them.  The hold is bounded by 2^16 sequence numbers and by 64 MB of
+    payload (lsp.cpp on_data): past 64 MB new early messages are dropped
+    un-acked.  3,000 x 30 KB = 86 MB are sent, a few at a time; the server
+    acks at most 64 MB worth and its RSS grows by less than what was sent."""
+    make = subprocess.run(["make", "-s", "-C", ROOT, "p1_amd/p1server"], check=True)
+    assert make.returncode == 0
+    srv = subprocess.Popen([os.path.join(ROOT, "p1_amd", "p1server"), "--epoch-millis", "2000", "--epoch-limit", "50",
+                            "lsp", "0"], stdout=subprocess.PIPE, text=True)
+    try:
+        line = srv.stdout.readline()
+        assert line.startswith("Server listening on port"), line
+        addr = ("127.0.0.1", int(line.split()[-1]))
+        s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 22)
+        s.settimeout(2.0)
+        s.sendto(lsp_msg(0, 0, 0, 0, None), addr)
+        conn = json.loads(s.recv(65536))["ConnID"]
+        time.sleep(0.2)
+        rss0 = rss_kb(srv.pid)
+        payload = os.urandom(30000)
+        p64 = b64(payload)
+        acked = set()
+
+        def drain(want, deadline):
+            while len(acked) < want and time.monotonic() < deadline:
+                try:
+                    m = json.loads(s.recv(65536))
+                except socket.timeout:
+                    return
+                except ValueError:
+                    continue
+                if m.get("Type") == 2 and m.get("SeqNum", 0) >= 2:
+                    acked.add(m["SeqNum"])
+
+        s.settimeout(0.02)
+        sent = 0
+        for seq in range(2, 3002):  # seq 1 never sent: everything is early
+            s.sendto(lsp_msg(1, conn, seq, len(payload), p64), addr)
+            sent += 1
+            if sent % 4 == 0:  # a few 40 KB datagrams at a time: the socket buffers are small
+                drain(sent, time.monotonic() + 0.05)
+        drain(sent, time.monotonic() + 0.5)
+        grown_mb = (rss_kb(srv.pid) - rss0) / 1024
+        held_mb = len(acked) * len(payload) / 2**20
+        assert srv.poll() is None
+        print("acked", len(acked), "held MB", round(held_mb, 1), "RSS growth MB", round(grown_mb, 1))
+        assert 2000 < len(acked) and held_mb <= 64.0 + 0.1, (len(acked), held_mb)
+        assert grown_mb < 80, grown_mb  # 86 MB were sent
+    finally:
+        srv.kill()
+        srv.wait()
