@@ -2,7 +2,7 @@
 coverage-guided fuzzer and against an independent JSON grammar.
 
 - `make fuzz` builds tests/fuzz/fuzz_codecs.cpp with libFuzzer + ASan +
-  UBSan; here it runs for 10 s from the seeds in tests/fuzz/seeds (a longer
+  UBSan; here it runs for 6 s from the seeds in tests/fuzz/seeds (a longer
   run: tools/fuzz.sh).  Properties: no sanitizer report; a syntax error
   leaves the message untouched; any other input re-encodes to an error-free
   fixed point; base64 decode(encode(decode(s))) == decode(s).
@@ -26,11 +26,11 @@ SANCXX = "/opt/rocm/lib/llvm/bin/clang++"
 
 
 @pytest.mark.skipif(not os.path.exists(SANCXX), reason="ROCm clang (libFuzzer runtime) not present")
-def test_codec_fuzzer_10s(tmp_path):
+def test_codec_fuzzer_6s(tmp_path):
     subprocess.run(["make", "-s", "-C", ROOT, "fuzz"], check=True, stdout=subprocess.DEVNULL)
     corpus = tmp_path / "corpus"
     shutil.copytree(os.path.join(ROOT, "tests", "fuzz", "seeds"), corpus)
-    r = subprocess.run([FUZZ, "-max_total_time=10", "-print_final_stats=1", "-max_len=4096", str(corpus)],
+    r = subprocess.run([FUZZ, "-max_total_time=6", "-print_final_stats=1", "-max_len=4096", str(corpus)],
                        capture_output=True, text=True, timeout=120, cwd=tmp_path)
     assert r.returncode == 0, r.stderr[-4000:]
     runs = [ln for ln in r.stderr.splitlines() if ln.startswith("stat::number_of_executed_units")]
@@ -38,13 +38,13 @@ def test_codec_fuzzer_10s(tmp_path):
 
 
 @pytest.mark.skipif(not os.path.exists(SANCXX), reason="ROCm clang (libFuzzer runtime) not present")
-def test_planner_fuzzer_10s(tmp_path):
+def test_planner_fuzzer_6s(tmp_path):
     """planner.hpp (make_plan, plan_shards) on fuzzer-chosen lengths, ranges
     near decade edges and the u64 top, shard counts and planner switches
     (tests/fuzz/fuzz_planner.cpp): every plan succeeds and hashes exactly
     upper-lower+1 nonces; shards are in order, contiguous and cover the range."""
     subprocess.run(["make", "-s", "-C", ROOT, "fuzz"], check=True, stdout=subprocess.DEVNULL)
-    r = subprocess.run([os.path.join(ROOT, "build", "san", "fuzz_planner"), "-max_total_time=10", "-seed=440",
+    r = subprocess.run([os.path.join(ROOT, "build", "san", "fuzz_planner"), "-max_total_time=6", "-seed=440",
                         "-print_final_stats=1"], capture_output=True, text=True, timeout=120, cwd=tmp_path)
     assert r.returncode == 0, r.stderr[-4000:]
     runs = [ln for ln in r.stderr.splitlines() if ln.startswith("stat::number_of_executed_units")]
