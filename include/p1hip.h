@@ -165,6 +165,23 @@ typedef struct {
 
 int p1hip_device_info(int index, p1hip_device_info_t *out);
 
+/* The RCCL communicator of device `index` (as for p1hip_get_device_stats),
+ * as RCCL itself reports it: *nranks = ncclCommCount, *rank =
+ * ncclCommUserRank.  A device without a communicator (one device, or the
+ * P1HIP_NO_RCCL host combine) gives *nranks = 0, *rank = -1 with rc 0.  With
+ * N devices opened by p1hip_init(N) every device reports N ranks and the
+ * ranks are 0..N-1 once each: the all-gather inside p1hip_scan spans them
+ * all (bench.py refuses to time an N-GPU run for which this does not hold). */
+int p1hip_comm_info(int index, int *nranks, int *rank);
+
+/* Layout version of the structs above.  A consumer compiled against this
+ * header checks p1hip_abi_version() == P1HIP_ABI_VERSION before reading any
+ * p1hip_*_t the library fills in.  History: 4 = p1hip 0.4 (fast_kernel_ms
+ * removed from p1hip_stats_t, so the fields after fast_alg_ops moved); 5 =
+ * p1hip 0.5 (p1hip_comm_info and this query added; the structs are as in 4). */
+#define P1HIP_ABI_VERSION 5
+int p1hip_abi_version(void);
+
 const char *p1hip_last_error(void);
 const char *p1hip_version(void);
 

@@ -23,6 +23,9 @@ from ._lib import (  # noqa: F401
     reset_stats,
     device_count,
     device_info,
+    comm_info,
+    abi_version,
+    ABI_VERSION,
     test_knobs,
     shutdown,
     version,

@@ -104,6 +104,8 @@ SIGNATURES = [
     ("p1hip_get_device_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(DeviceStats)]),
     ("p1hip_device_count", ctypes.c_int, []),
     ("p1hip_device_info", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(DeviceInfo)]),
+    ("p1hip_comm_info", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    ("p1hip_abi_version", ctypes.c_int, []),
     ("p1hip_test_knobs", ctypes.c_char_p, []),
     ("p1hip_last_error", ctypes.c_char_p, []),
     ("p1hip_version", ctypes.c_char_p, []),
@@ -124,6 +126,9 @@ def load(path=None):
         fn = getattr(lib, name)  # AttributeError if the export is missing
         fn.restype = res
         fn.argtypes = args
+    if lib.p1hip_abi_version() != ABI_VERSION:
+        raise P1HipError(-100, f"{p}: ABI version {lib.p1hip_abi_version()}, this binding reads version "
+                               f"{ABI_VERSION} structs (rebuild the library)")
     if path is None:
         _LIB = lib
     return lib
@@ -209,6 +214,23 @@ def device_info(index):
     s = DeviceInfo()
     _check(load().p1hip_device_info(int(index), ctypes.byref(s)))
     return s.as_dict()
+
+
+def comm_info(index):
+    """(nranks, rank) of device `index`'s RCCL communicator as RCCL reports
+    it (p1hip_comm_info: ncclCommCount / ncclCommUserRank); (0, -1) for a
+    device without one."""
+    n, r = ctypes.c_int(0), ctypes.c_int(-1)
+    _check(load().p1hip_comm_info(int(index), ctypes.byref(n), ctypes.byref(r)))
+    return n.value, r.value
+
+
+# include/p1hip.h P1HIP_ABI_VERSION: the struct layouts this module declares
+ABI_VERSION = 5
+
+
+def abi_version():
+    return load().p1hip_abi_version()
 
 
 def test_knobs():

@@ -971,9 +971,29 @@ int p1hip_get_device_stats(int index, p1hip_device_stats_t* out) {
   return P1HIP_OK;
 }
 
+int p1hip_comm_info(int index, int* nranks, int* rank) {
+  if (!nranks || !rank) return fail(P1HIP_ERR_ARGS, "null comm-info pointer");
+  *nranks = 0;
+  *rank = -1;
+  Runtime& R = rt();
+  std::lock_guard<std::mutex> g(R.mu);
+  if (index < 0 || (size_t)index >= R.devs.size()) return fail(P1HIP_ERR_ARGS, "device index out of range");
+  const Dev& d = R.devs[(size_t)index];
+  if (!d.comm) return P1HIP_OK;  // one device without P1HIP_FORCE_RCCL, or host combine
+  // what RCCL itself says, not what init asked for
+  int count = 0, user = -1;
+  NCCLCHK(ncclCommCount(d.comm, &count));
+  NCCLCHK(ncclCommUserRank(d.comm, &user));
+  *nranks = count;
+  *rank = user;
+  return P1HIP_OK;
+}
+
+int p1hip_abi_version(void) { return P1HIP_ABI_VERSION; }
+
 const char* p1hip_last_error(void) { return g_err.c_str(); }
 
-const char* p1hip_version(void) { return "p1hip 0.4 gfx950"; }
+const char* p1hip_version(void) { return "p1hip 0.5 gfx950"; }
 
 const char* p1hip_test_knobs(void) {
   static thread_local std::string s;

@@ -140,8 +140,11 @@ def test_roofline_assembly_rejects_frac_above_one():
     cfg = bench.CONFIGS["c4"]
     with pytest.raises(bench.RooflineError):
         bench.assemble_roofline("c4", cfg, _stats(1 << 38, 2000.0), 1)
-    with pytest.raises(bench.RooflineError):
-        bench.assemble_roofline("c2", bench.CONFIGS["c2"], _stats(1 << 32, 117.0), 1, rocprof=(30e6, "z"))
+    # a committed rocprof average too short for the work (a stale profile) is
+    # flagged beside the line, not a refusal of this run's own numbers
+    roof = bench.assemble_roofline("c2", bench.CONFIGS["c2"], _stats(1 << 32, 117.0), 1, rocprof=(30e6, "z"))
+    assert "frac_rocprof" not in roof and roof["stale_profile"]["frac_rocprof"] > 1.0
+    assert 0.6 < roof["frac"] < 0.7
     with pytest.raises(bench.RooflineError):
         bench.check_fracs({"a": {"frac_x": 1.01}}, 1)
     bench.check_fracs({"a": {"frac_x": 1.01}}, 2)  # 2-block: the algorithmic count is not a utilisation
@@ -200,3 +203,37 @@ def test_scaling_expectation_for_the_driver_shapes():
         assert e and e["slowest_shard_over_mean"] < 1.01 and len(e["shard_kernel_ms"]) == n
     assert 290 < bench.scaling_expectation("c4", 8)["implied_GH_s"] < 300
     assert bench.scaling_expectation("c4", 1) is None and bench.scaling_expectation("c2", 8) is None
+
+
+def test_library_topology_reports_what_rccl_says():
+    """a library-mode N-GPU record carries each device's
+    communicator size and rank as RCCL reports them (p1hip_comm_info) and a
+    world_size taken from them, not a constant."""
+    t = bench.library_topology("library", 8, [(8, r) for r in (3, 0, 1, 2, 4, 5, 6, 7)])
+    assert t["world_size"] == 8 and t["ranks_in_gather"] == 8 and t["processes"] == 1
+    assert t["rccl_ranks"] == [8] * 8 and sorted(t["rccl_rank"]) == list(range(8))
+    t1 = bench.library_topology("single", 1, [(0, -1)])
+    assert t1["world_size"] == 1 and t1["ranks_in_gather"] is None and t1["rccl_ranks"] == [0]
+    assert t1["backend"] is None
+
+
+@pytest.mark.parametrize("comms", [
+    [(1, 0), (1, 0)],            # two one-rank communicators: no cross-GPU gather
+    [(2, 0), (2, 0)],            # one rank twice
+    [(0, -1), (0, -1)],          # host combine (P1HIP_NO_RCCL)
+    [(4, 0), (4, 1)],            # a communicator larger than the run
+    [(2, 0)],                    # fewer devices than --gpus
+])
+def test_library_topology_refuses_a_gather_that_does_not_span_the_gpus(comms):
+    with pytest.raises(bench.TopologyError):
+        bench.library_topology("library", 2, comms)
+
+
+def test_bench_exits_5_on_a_bad_communicator():
+    """main() queries p1_amd.comm_info after init and exits 5 before timing
+    when library_topology refuses."""
+    import inspect
+
+    src = inspect.getsource(bench.main)
+    assert "comm_info" in src and "sys.exit(5)" in src
+    assert src.index("sys.exit(5)") < src.index("timed_steps(")

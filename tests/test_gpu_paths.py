@@ -289,6 +289,25 @@ def test_rccl_allgather_one_device(reinit, oracle_mod):
     for m, lo, hi in [(b"bradfitz", 0, 9999), (b"msg", 0, 2), (b"msg", 7, 3), (b"x" * 70, 10**9 - 3000, 10**9 + 3000)]:
         assert g.scan(m, lo, hi) == oracle_mod.scan(m, lo, hi, threads=8)
     assert g.scan("bradfitz", 0, (1 << 32) - 1) == (5256245051, 1626825724)
+    # the communicator as RCCL reports it
+    assert g.comm_info(0) == (1, 0)
+
+
+def test_comm_info_without_a_communicator(reinit):
+    """One device without P1HIP_FORCE_RCCL, and the host combine of two
+    logical devices, have no communicator: (0, -1); bench.py's
+    library_topology refuses such a pair as a 2-GPU run."""
+    import bench
+
+    g = reinit((0,))
+    assert g.comm_info(0) == (0, -1)
+    with pytest.raises(g.P1HipError):
+        g.comm_info(1)
+    g = reinit((0, 0), P1HIP_NO_RCCL=1)
+    comms = [g.comm_info(0), g.comm_info(1)]
+    assert comms == [(0, -1), (0, -1)]
+    with pytest.raises(bench.TopologyError):
+        bench.library_topology("library", 2, comms)
 
 
 def test_failure_on_one_device_does_not_hang(reinit, oracle_mod):

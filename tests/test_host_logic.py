@@ -235,6 +235,20 @@ def test_capi_exports_every_header_symbol():
     assert p1_amd.version().startswith("p1hip")
 
 
+def test_capi_abi_version_and_comm_info_without_devices():
+    """ADVICE r04 (struct layout): the library reports the header's
+    P1HIP_ABI_VERSION and the binding refuses another one; comm_info on a
+    device that is not open is an argument error, never a made-up size."""
+    import p1_amd
+
+    with open(os.path.join(ROOT, "include", "p1hip.h")) as f:
+        want = int(re.search(r"#define P1HIP_ABI_VERSION (\d+)", f.read()).group(1))
+    assert p1_amd.abi_version() == want == p1_amd.ABI_VERSION
+    with pytest.raises(p1_amd.P1HipError) as ei:
+        p1_amd.comm_info(0)
+    assert ei.value.rc == -4
+
+
 def test_capi_no_device_fails_loudly():
     """Without a GPU the product path raises; it never falls back to a CPU hash."""
     import p1_amd
