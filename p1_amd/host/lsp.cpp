@@ -114,25 +114,36 @@ void on_ack(Peer& p, int64_t seq, int window, const SendFn& send) {
 // window of them, so more than kMaxEarlyBytes of payload held ahead of
 // `expect` is a faulty peer, and a new early message beyond it is dropped
 // un-acked too (64 KB datagrams x 2^16 sequence numbers would be 4 GB).
+// A server also caps the early bytes of ALL its connections together
+// (kMaxEarlyBytesAll, `pool`): a connection costs one unauthenticated Connect,
+// so a per-connection cap alone would let many of them hold 64 MB each.
 constexpr int64_t kMaxEarly = 1 << 16;
 constexpr size_t kMaxEarlyBytes = 64u << 20;
-void on_data(Peer& p, Message& m, int window, const SendFn& send, const DeliverFn& deliver) {
+constexpr size_t kMaxEarlyBytesAll = 256u << 20;
+void on_data(Peer& p, Message& m, int window, const SendFn& send, const DeliverFn& deliver, size_t* pool = nullptr) {
   (void)window;
   if (m.SeqNum >= p.expect + kMaxEarly) return;
-  if (m.SeqNum > p.expect && !p.early.count(m.SeqNum) && p.early_bytes + m.Payload.size() > kMaxEarlyBytes) return;
+  if (m.SeqNum > p.expect && !p.early.count(m.SeqNum) &&
+      (p.early_bytes + m.Payload.size() > kMaxEarlyBytes ||
+       (pool && *pool + m.Payload.size() > kMaxEarlyBytesAll)))
+    return;
   send(NewAck(p.conn_id, m.SeqNum));
   p.got_data = true;
   if (m.SeqNum < p.expect) return;
   std::string payload(m.Payload.begin(), m.Payload.end());
   if (m.SeqNum > p.expect) {
     const size_t n = payload.size();
-    if (p.early.emplace(m.SeqNum, std::move(payload)).second) p.early_bytes += n;
+    if (p.early.emplace(m.SeqNum, std::move(payload)).second) {
+      p.early_bytes += n;
+      if (pool) *pool += n;
+    }
     return;
   }
   deliver(std::move(payload));
   p.expect++;
   for (auto it = p.early.find(p.expect); it != p.early.end(); it = p.early.find(p.expect)) {
     p.early_bytes -= it->second.size();
+    if (pool) *pool -= it->second.size();
     deliver(std::move(it->second));
     p.early.erase(it);
     p.expect++;
@@ -258,8 +269,11 @@ class ClientImpl : public Client {
   bool Connect(std::string* err) {
     {
       std::lock_guard<std::mutex> g(mu_);
-      p_.copies = prm_.Copies > 1 ? prm_.Copies : 1;
-      for (int i = 0; i < p_.copies; ++i) send_(NewConnect());
+      p_.copies = prm_.Copies > 1 ? prm_.Copies : 1;  // Data only
+      // one Connect per attempt by default: a reference server opens a
+      // connection per Connect datagram (Params::ConnectCopies)
+      const int cc = prm_.ConnectCopies > 1 ? prm_.ConnectCopies : 1;
+      for (int i = 0; i < cc; ++i) send_(NewConnect());
     }
     loop_->Start();
     std::unique_lock<std::mutex> lk(mu_);
@@ -492,9 +506,12 @@ class ServerImpl : public Server {
     } else if (m.Type == MsgData) {
       const bool hide = c.closing;
       const int64_t id = c.p.conn_id;
-      on_data(c.p, m, prm_.WindowSize, send, [this, hide, id](std::string&& s) {
-        if (!hide) inbox_.push_back({id, std::move(s), false});
-      });
+      on_data(
+          c.p, m, prm_.WindowSize, send,
+          [this, hide, id](std::string&& s) {
+            if (!hide) inbox_.push_back({id, std::move(s), false});
+          },
+          &early_all_);
       cv_.notify_all();
     }
   }
@@ -519,6 +536,7 @@ class ServerImpl : public Server {
       if (c.p.lost && closing_all_ && !c.p.out.empty()) lost_while_closing_ = true;
       auto a = by_addr_.find(c.p.addr);
       if (a != by_addr_.end() && a->second == c.p.conn_id) by_addr_.erase(a);
+      early_all_ -= c.p.early_bytes;  // its held-back data leaves with it
       it = conns_.erase(it);
       changed = true;
     }
@@ -540,6 +558,7 @@ class ServerImpl : public Server {
   std::map<lspnet::UDPAddr, int64_t> by_addr_;
   std::deque<Event> inbox_;
   int64_t next_id_ = 1;
+  size_t early_all_ = 0;  // early bytes held by all connections (kMaxEarlyBytesAll)
   bool closing_all_ = false, lost_while_closing_ = false, closed_ = false;
   std::unique_ptr<Loop> loop_;  // last: stopped first
 };

@@ -46,13 +46,24 @@ struct Params {  // params.go:14-26
   int EpochLimit = DefaultEpochLimit;
   int EpochMillis = DefaultEpochMillis;
   int WindowSize = DefaultWindowSize;
-  // Not in the reference: datagrams per FIRST transmission of a Connect, of
-  // a new connection's Ack and of a Data message (epoch resends go out
-  // once).  1 = the reference's behaviour.  Wire-compatible: receivers ack
-  // every copy and deliver each sequence number once, so at a drop rate p a
-  // message is late by a whole epoch only with probability p^Copies instead
-  // of p.  The bitcoin programs use DefaultAppCopies.
+  // Not in the reference: datagrams per FIRST transmission of a Data
+  // message and of a new connection's Ack (epoch resends go out once).
+  // 1 = the reference's behaviour.  Safe against a reference peer: its
+  // receive path acks every Data copy and delivers each sequence number once
+  // (lsp/common.go:37-42), and its client takes the first Ack(id, 0) of a
+  // connect and ignores the rest; so at a drop rate p a message is late by a
+  // whole epoch only with probability p^Copies instead of p.  The bitcoin
+  // programs use DefaultAppCopies.
   int Copies = 1;
+  // Not in the reference: datagrams per Connect request (first transmission;
+  // the epoch resend of an unanswered Connect goes out once, as in
+  // client_impl.go).  Keep it 1 against a reference server: server_impl.go
+  // opens a NEW connection for every Connect datagram it reads
+  // (server_impl.go:117-137,199-200; it has no per-address lookup), so each
+  // extra copy leaves a phantom connection there until its epoch limit.
+  // This library's server answers duplicate Connects from one address with
+  // the same id, so a value > 1 is harmless only against it.
+  int ConnectCopies = 1;
   std::string String() const;  // params.go:41-44
 };
 

@@ -3,7 +3,7 @@
 // "Result <hash> <nonce>", or "Disconnected" if the connection is lost.
 //
 //   p1client <host:port> <message> <maxNonce> [--epoch-limit K]
-//            [--epoch-millis M] [--window W] [--copies K]
+//            [--epoch-millis M] [--window W] [--copies K] [--connect-copies K]
 // Reference: /root/reference/src/github.com/cmu440/bitcoin/client/client.go
 // P1LSP_* env vars inject loss (lspnet.hpp).
 #include <errno.h>
@@ -32,6 +32,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--epoch-millis") && i + 1 < argc) prm.EpochMillis = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--window") && i + 1 < argc) prm.WindowSize = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--copies") && i + 1 < argc) prm.Copies = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--connect-copies") && i + 1 < argc) prm.ConnectCopies = atoi(argv[++i]);
     else return 2;
   }
   const std::string hostport = argv[1], message = argv[2];

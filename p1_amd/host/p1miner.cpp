@@ -3,7 +3,7 @@
 // Requests/results are encoding/json bitcoin.Message bytes (miner.go:55,66).
 //
 //   p1miner lsp <host:port> [--device N] [--chunk C] [--epoch-limit K]
-//           [--epoch-millis M] [--window W] [--copies K]
+//           [--epoch-millis M] [--window W] [--copies K] [--connect-copies K]
 //                                        miner.go:13-73: connect, send Join,
 //                                        then Read -> scan -> Write until the
 //                                        connection is lost.  The scan runs on
@@ -51,7 +51,7 @@ static int usage() {
   fprintf(stderr,
           "usage: p1miner scan <msg> <lower> <upper> | hash <msg> <nonce> | "
           "serve [--device N] [--chunk C] | lsp <host:port> [--device N] [--chunk C] [--epoch-limit K] "
-          "[--epoch-millis M] [--window W] [--copies K] | json | lsp-json | lsp-wrap <connID> <seq> | lsp-unwrap\n");
+          "[--epoch-millis M] [--window W] [--copies K] [--connect-copies K] | json | lsp-json | lsp-wrap <connID> <seq> | lsp-unwrap\n");
   return 2;
 }
 
@@ -79,6 +79,7 @@ static int run_lsp(int argc, char** argv) {
     else if (!strcmp(argv[i], "--epoch-millis") && i + 1 < argc) prm.EpochMillis = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--window") && i + 1 < argc) prm.WindowSize = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--copies") && i + 1 < argc) prm.Copies = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--connect-copies") && i + 1 < argc) prm.ConnectCopies = atoi(argv[++i]);
     else return usage();
   }
   // open the GPU before joining, so the first request does not pay for it

@@ -2,7 +2,7 @@
 // loop of miner.go:13-73 over this repository's LSP, answering every request
 // with the oracle (oracle/libp1oracle.so, the CPU checker) instead of the GPU.
 //
-//   lsp_fake_miner <host:port> [--epoch-limit K] [--epoch-millis M] [--window W] [--copies K]
+//   lsp_fake_miner <host:port> [--epoch-limit K] [--epoch-millis M] [--window W] [--copies K] [--connect-copies K]
 // FAKE_DIE_AFTER=n: after answering n requests, read the next one and exit
 // without answering or closing (a miner the server must declare lost).
 // FAKE_LOG=path: append "lower upper" of every request received (tests check
@@ -33,6 +33,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--epoch-millis") && i + 1 < argc) prm.EpochMillis = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--window") && i + 1 < argc) prm.WindowSize = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--copies") && i + 1 < argc) prm.Copies = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--connect-copies") && i + 1 < argc) prm.ConnectCopies = atoi(argv[++i]);
     else return 2;
   }
   const char* die = getenv("FAKE_DIE_AFTER");

@@ -4,7 +4,8 @@
 double miner and the scheduler unit test with each sanitizer (ROCm's clang;
 DESIGN.md §6 "Host code under sanitizers").  Here the reference LSP
 scenarios run under the two builds (half under each) with the production
-default of two copies per first transmission, the scheduler unit test
+default of three copies per first Data transmission (lsp::DefaultAppCopies),
+the scheduler unit test
 under ASan, and a whole
 server + miners + client system under loss under both; a run passes only
 if it succeeds AND leaves no sanitizer report file.  tools/sanitize.sh
@@ -51,11 +52,12 @@ def test_lsp_scenarios_under_sanitizer(kind, tmp_path):
     names = subprocess.run([drv, "--list"], capture_output=True, text=True, check=True, env=env).stdout.split()
     assert len(names) == 48
     # every other scenario keeps the CPU suite short; tools/sanitize.sh runs
-    # all 48 at 1 and 2 copies under both sanitizers
+    # all 48 at 1 and 2 copies under both sanitizers; here the programs'
+    # default, lsp::DefaultAppCopies = 3
     names = names[::2] if kind == "tsan" else names[1::2]
 
     def run(name):
-        r = subprocess.run([drv, "--copies", "2", name], capture_output=True, text=True, timeout=240, env=env)
+        r = subprocess.run([drv, "--copies", "3", name], capture_output=True, text=True, timeout=240, env=env)
         return name, r.returncode, r.stdout + r.stderr
 
     with ThreadPoolExecutor(max_workers=6) as ex:
