@@ -89,6 +89,35 @@ def test_chunkloop_on_gpu(tmp_path, oracle_mod):
             assert "cpu_chunks=0" not in r.stdout
 
 
+def test_go_binding_plan_shards_edges(tmp_path):
+    """INTEGRATION.md's gpu.PlanShards through the C ABI as the binding calls
+    it: n = 0 and n < 0 return the library's
+    P1HIP_ERR_ARGS with its message (the binding must not index &f[0]), and
+    n >= 1 gives n in-order contiguous shards over [lower, upper]; lower >
+    upper gives n empty shards.  Host only (no device)."""
+    exe = tmp_path / "capi_plan_shards"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror",
+                    "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "capi_plan_shards.c"),
+                    "-L", os.path.join(ROOT, "p1_amd"), "-lp1hip", f"-Wl,-rpath,{os.path.join(ROOT, 'p1_amd')}",
+                    "-o", str(exe)], check=True)
+
+    def run(*a):
+        r = subprocess.run([str(exe)] + [str(x) for x in a], capture_output=True, text=True, timeout=60)
+        return r.returncode, r.stdout.splitlines()
+
+    for n in (0, -1, -(2 ** 31)):
+        rc, out = run("bradfitz", 0, 9999, n)
+        assert rc == 0 and out[0].startswith("rc -4 ") and "n <= 0" in out[0], out
+    rc, out = run("", 0, 9999, 0)  # empty message: NULL msg pointer with length 0 is valid
+    assert rc == 0 and out[0].startswith("rc -4 "), out
+    for msg, lo, hi, n in [("bradfitz", 0, (1 << 38) - 1, 8), ("bradfitz", 0, 9999, 1), ("x" * 70, 10, 12, 8),
+                           ("", 0, 0, 3), ("bradfitz", 2 ** 64 - 100, 2 ** 64 - 1, 4)]:
+        rc, out = run(msg, lo, hi, n)
+        assert rc == 0 and out[0] == "ok" and len(out) == n + 1, (msg, lo, hi, n, out)
+    rc, out = run("bradfitz", 7, 3, 5)  # lower > upper: n empty shards, rc 0
+    assert rc == 0 and out[0] == "ok" and all(line.endswith(" 0") for line in out[1:]) and len(out) == 6
+
+
 SAN_STRESS = os.path.join(ROOT, "tools", "san", "capi_san_stress")
 
 
