@@ -23,6 +23,10 @@ BUILD := build
 all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios \
      tools/lsp_fake_miner tools/queue_ctl tools/wcal tools/vbank
 
+# The assembly and object stages are intermediates: once the code object
+# exists, a tree without them (the GPU box's copy leaves the 16 MB of .s out,
+# .gpurunignore) does not recompile the kernels unless a source is newer.
+.SECONDARY: $(BUILD)/p1hip_kernels.s $(BUILD)/p1hip_kernels.post.s $(BUILD)/p1hip_kernels.o
 $(BUILD)/p1hip_kernels.s: $(CSRC)/p1hip_kernels.hip $(DEVHDRS) Makefile
 	mkdir -p $(BUILD)
 	$(HIPCC) $(DEVFLAGS) -S -o $@ $(CSRC)/p1hip_kernels.hip

@@ -118,19 +118,42 @@ def test_go_binding_plan_shards_edges(tmp_path):
     assert rc == 0 and out[0] == "ok" and all(line.endswith(" 0") for line in out[1:]) and len(out) == 6
 
 
-SAN_STRESS = os.path.join(ROOT, "tools", "san", "capi_san_stress")
+SAN_DIR = os.path.join(ROOT, "tools", "san")
+SAN_STRESS = os.path.join(SAN_DIR, "capi_san_stress")
+# what `make sanitize-lib` produces (Makefile SANLIB); all of it is rebuilt
+# from this tree's sources by the test itself, never taken as found
+SAN_OUTPUTS = ["p1hip_host.o", "libp1hip.so", "capi_san_stress", "p1miner"]
+
+
+def build_sanitize_lib():
+    """Delete every ASan artefact and rebuild it from the checked-out
+    sources (a binary pushed from elsewhere, or one
+    older than the sources, must never be what the test runs).  Host code
+    only, ~25 s; the kernels are the shipped code object
+    (build/p1hip_kernels_blob.o, which `make all` made for libp1hip.so)."""
+    for f in SAN_OUTPUTS:
+        try:
+            os.remove(os.path.join(SAN_DIR, f))
+        except FileNotFoundError:
+            pass
+    jobs = str(min(16, os.cpu_count() or 1))
+    r = subprocess.run(["make", "-s", "-C", ROOT, "-j", jobs, "sanitize-lib"], capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert os.path.exists(SAN_STRESS)
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(not os.path.exists(SAN_STRESS), reason="`make sanitize-lib` not built (ASan host runtime)")
 def test_host_runtime_under_asan(tmp_path):
     """The library's host runtime built with ASan + UBSan on the host side
-    (`make sanitize-lib`; the kernels are the shipped code object) drives
-    real scans for 40 s: planner, argument errors, exact and property-checked
-    random scans, 4 host threads at once, the argmin on crafted pairs, 3
-    logical devices with host combine, launch / table / span caps, an
-    injected device failure and recovery, re-init cycles
-    (tests/capi_san_stress.cpp).  Passes only with rc 0 and no report file."""
+    (`make sanitize-lib`, rebuilt here from the tree's sources; the kernels
+    are the shipped code object) drives real scans for 40 s: planner,
+    argument errors, exact and property-checked random scans, 4 host threads
+    at once, the argmin on crafted pairs, 3 logical devices with host
+    combine, launch / table / span caps, an injected device failure and
+    recovery, re-init cycles (tests/capi_san_stress.cpp).  Passes only with
+    rc 0 and no report file."""
+    build_sanitize_lib()
     env = dict(os.environ,
                ASAN_OPTIONS=f"detect_leaks=1:log_path={tmp_path}/asan",
                LSAN_OPTIONS=f"suppressions={os.path.join(ROOT, 'tests', 'lsan_rocm.supp')}:print_suppressions=0",
