@@ -130,7 +130,7 @@ $(SANDIR)/%/lsp_fake_miner: tests/lsp/lsp_fake_miner.cpp $(HOSTSRC) $(HOSTHDR) o
 # are the shipped code object) and its GPU stress driver; in tools/san, not
 # build/, so that they travel to the GPU box with the tree
 SANLIB := tools/san
-sanitize-lib: $(SANLIB)/libp1hip.so $(SANLIB)/capi_san_stress $(SANLIB)/p1miner
+sanitize-lib: $(SANLIB)/libp1hip.so $(SANLIB)/capi_san_stress $(SANLIB)/p1miner tools/asan_teardown
 $(SANLIB)/p1miner: p1_amd/host/p1miner.cpp p1_amd/host/miner_gpu.cpp $(HOSTSRC) $(HOSTHDR) $(SANLIB)/libp1hip.so
 	$(SANCXX) $(SANBASE) $(SAN_asan) -o $@ p1_amd/host/p1miner.cpp p1_amd/host/miner_gpu.cpp $(HOSTSRC) -L$(SANLIB) -lp1hip \
 	    -Wl,-rpath,'$$ORIGIN'
@@ -143,6 +143,12 @@ $(SANLIB)/libp1hip.so: $(SANLIB)/p1hip_host.o $(BUILD)/p1hip_kernels_blob.o
 $(SANLIB)/capi_san_stress: tests/capi_san_stress.cpp include/p1hip.h $(SANLIB)/libp1hip.so oracle
 	$(SANCXX) $(SANBASE) $(SAN_asan) -Iinclude -o $@ tests/capi_san_stress.cpp -L$(SANLIB) -lp1hip \
 	    -Wl,-rpath,'$$ORIGIN' -Loracle -lp1oracle -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+# measurement program: does ROCm's ASan runtime abort at exit without
+# libp1hip at all (the r04p teardown CHECK)
+tools/asan_teardown: tools/asan_teardown.cpp
+	$(HIPCC) -O1 -g -std=c++17 -fno-omit-frame-pointer -Xarch_host -fsanitize=address -o $@ tools/asan_teardown.cpp \
+	    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 # the same under TSan (the device threads, barriers and the combine of a
 # multi-device scan; the HIP runtime itself is not instrumented)

@@ -109,3 +109,81 @@ def test_post_pass_assembles_with_parity(tmp_path):
             for m in re.finditer(r"^\s+(\w+).*//\s*([0-9A-F]+):\s*((?:[0-9A-F]{8}\s*)+)$", dis, re.M)]
     loop = [a for a in addr if a[2] in ("v_alignbit_b32", "v_bitop3_b32", "v_add3_u32", "v_add_u32_e64")]
     assert len(loop) == 5 and all(a % 8 == 4 for a, n, _ in loop if n == 2), addr
+
+
+# ---------------------------------------------------------------------------
+# the roofline (0.649 on c4) sits at the floor of the
+# loop mix, so a toolchain or post-pass change that lengthens the per-nonce
+# loops is the only way left to lose it.  These counts are read off the
+# shipped code object on the CPU and compared with the per-variant report
+# (profiles/r03f_variant_report.jsonl, tools/variant_report.py: each variant
+# built alone through the same pipeline).  The full kernel's register
+# allocation moves a loop by up to 3 instructions either way against its
+# single-variant build, hence the tolerance (3 VALU = 0.25% of a loop).
+# ---------------------------------------------------------------------------
+VARIANT_REPORT = os.path.join(ROOT, "profiles", "r03f_variant_report.jsonl")
+# (FV, MODE, TRAIL): (half-rate A, full-rate B) VALU per nonce in its loop,
+# for the decades that carry the bench workloads (bench.fast_variant)
+PINNED_LOOPS = {
+    (4, 6, False): (697, 500),   # c2 d = 10 (77% of configs[1]), c4 d = 10
+    (3, 3, False): (697, 500),   # c2 d = 9 (21%)
+    (4, 4, False): (684, 489),   # c4 d = 12 (64% of configs[3])
+    (4, 1, False): (699, 503),   # c4 d = 11 (33%)
+    (0, 5, False): (508, 381),   # c3 MODE 5, d = 9..11 (99% of configs[2])
+    (15, 7, False): (505, 384),  # c3 MODE 7, d = 8
+}
+LOOP_TOL = 3
+
+
+@pytest.fixture(scope="module")
+def shipped_loops(codeobj):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import variant_report as vr
+
+    ins, inner, _ = vr.loops_of(codeobj)
+    per_nonce = [vr.mix(ins, *lp) for lp in inner]
+    return [m for m in per_nonce if m["valu"] > 500]  # one nonce per iteration (the rest: setup, reduce)
+
+
+def test_pinned_loop_counts_match_the_variant_report():
+    """The constants above are the committed report's own numbers."""
+    import json
+
+    rows = {}
+    for ln in open(VARIANT_REPORT):
+        d = json.loads(ln)
+        rows[tuple(d["variant"])] = (d["loop"]["half_rate_A"], d["loop"]["full_rate_B"])
+    for v, ab in PINNED_LOOPS.items():
+        assert rows[v] == ab, (v, rows[v], ab)
+    sys.path.insert(0, ROOT)
+    import bench
+
+    # ... and they are the variants the bench workloads' big decades run
+    assert bench.fast_variant(8, 10) == (4, 6, False) and bench.fast_variant(8, 9) == (3, 3, False)
+    assert bench.fast_variant(8, 12) == (4, 4, False) and bench.fast_variant(8, 11) == (4, 1, False)
+    assert bench.fast_variant(120, 10) == (0, 5, False) and bench.fast_variant(120, 8) == (15, 7, False)
+
+
+def test_shipped_hot_loops_are_no_longer_than_pinned(shipped_loops):
+    """Every pinned variant's loop is present in the shipped k_scan with its
+    half-rate and full-rate counts within LOOP_TOL, and every per-nonce loop
+    is free of memory instructions (no scratch spill reload per nonce)."""
+    assert len(shipped_loops) == 63, len(shipped_loops)  # one per fast variant (fast_variants.inc)
+    sigs = [(m["half_rate_A"], m["full_rate_B"]) for m in shipped_loops]
+    for v, (a, b) in PINNED_LOOPS.items():
+        near = [(x, y) for x, y in sigs if abs(x - a) <= LOOP_TOL and abs(y - b) <= LOOP_TOL]
+        assert near, (v, (a, b), sorted(sigs))
+        assert min(x + y for x, y in near) <= a + b + LOOP_TOL, (v, near)
+    assert all(m["other"] == 0 for m in shipped_loops), [m for m in shipped_loops if m["other"]]
+    # the post-pass parity rule holds inside every per-nonce loop
+    assert all(m["n8_at_4_mod_8"] >= m["n8"] - 2 for m in shipped_loops)
+
+
+def test_k_scan_registers_keep_four_waves(codeobj):
+    """<= 128 VGPRs (4 waves/SIMD, DESIGN.md 4 "Occupancy budget") and <= 106
+    SGPRs (the 64 round constants in SGPRs)."""
+    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", codeobj], capture_output=True, text=True,
+                           check=True).stdout
+    blk = notes[notes.index(".name:           k_scan\n"):]
+    get = lambda k: int(re.search(rf"\.{k}:\s+(\d+)", blk).group(1))  # noqa: E731
+    assert get("vgpr_count") <= 128 and get("sgpr_count") <= 106, (get("vgpr_count"), get("sgpr_count"))
