@@ -12,7 +12,9 @@ env: MINERS (8), NGPU (1), UPPER (2^36 - 1), CHUNK (2^32), WINDOW (8),
      a lost datagram is resent one epoch later, so at 5% drop the wall time
      holds whole epochs), COPIES (unset: the programs' default,
      lsp::DefaultAppCopies = 3; 1 = the reference protocol: datagrams per
-     first transmission); FAKE=1 runs the CPU oracle-backed miner double
+     first transmission), CONNECT_COPIES (unset: the programs' default
+     1, the reference's single Connect per attempt; lsp::Params::
+     ConnectCopies); FAKE=1 runs the CPU oracle-backed miner double
      (tools/lsp_fake_miner, test plumbing only) instead of p1miner
 Reference: server.go:45-170 (dispatch), miner.go:13-73, client.go:21."""
 import json
@@ -53,6 +55,9 @@ def main():
     copies = os.environ.get("COPIES")
     if copies:
         lsp += ["--copies", copies]
+    cc = os.environ.get("CONNECT_COPIES")
+    # the server never sends a Connect: only miners and the client take it
+    peer = ["--connect-copies", cc] if cc else []
     procs = []
     try:
         srv = subprocess.Popen([SERVER, "--chunk", str(chunk)] + lsp + ["lsp", "0"],
@@ -64,7 +69,7 @@ def main():
         hp = f"127.0.0.1:{int(line.split()[-1])}"
         fake = os.environ.get("FAKE") == "1"
         for i in range(miners):
-            argv = [FAKE, hp] + lsp if fake else [MINER, "lsp", hp, "--device", str(i % ngpu)] + lsp
+            argv = [FAKE, hp] + lsp + peer if fake else [MINER, "lsp", hp, "--device", str(i % ngpu)] + lsp + peer
             procs.append(subprocess.Popen(argv, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env))
 
         time.sleep(0.5)
@@ -74,7 +79,7 @@ def main():
 
         def request():
             t0 = time.perf_counter()
-            r = subprocess.run([CLIENT, hp, "bradfitz", str(upper)] + lsp, capture_output=True, text=True,
+            r = subprocess.run([CLIENT, hp, "bradfitz", str(upper)] + lsp + peer, capture_output=True, text=True,
                                timeout=600, env=env)
             dt = time.perf_counter() - t0
             if r.returncode != 0 or not r.stdout.startswith("Result"):
@@ -95,8 +100,9 @@ def main():
                         f"{miners} {'CPU oracle miner doubles' if fake else f'p1miner lsp processes on {ngpu} GPU(s)'}"
                         f"; LSP window {window}, {drop}% write drop in every process, "
                         f"{epoch or 'default (2000)'} ms epochs, "
-                        f"{copies or 'default (3)'} copies per first transmission",
-            "copies": int(copies) if copies else 3, "epoch_ms": int(epoch) if epoch else 2000, "miners": miners,
+                        f"{copies or 'default (3)'} copies per first Data transmission, "
+                        f"{cc or 'default (1)'} per Connect",
+            "copies": int(copies) if copies else 3, "connect_copies": int(cc) if cc else 1, "epoch_ms": int(epoch) if epoch else 2000, "miners": miners,
             "reps": reps, "wall_s": walls, "wall_s_median": med, "wall_s_max": max(walls),
             "wall_s_p90": sorted(walls)[min(len(walls) - 1, int(0.9 * len(walls)))], "warmup_wall_s": warm_s,
             "GH_s": (upper + 1) / med / 1e9,

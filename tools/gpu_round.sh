@@ -58,6 +58,22 @@ for lib in ${VARIANTS:-}; do
   n=$(basename "$lib" .so)
   P1HIP_LIB="$ROOT/$lib" step "bench_$n" 600 python "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu --no-by-config > "$OUT/${TAG}_bench_$n.json" 2> "$OUT/${TAG}_bench_$n.err"
 done
+if [ "${RUN_ASAN_TEARDOWN:-0}" = 1 ]; then
+  # whose free trips ROCm ASan's "!dev_runtime_unloaded_"
+  # at exit.  A HIP + RCCL program without libp1hip (tools/asan_teardown), then
+  # the library's stress driver through the normal exit path; every ASan
+  # report (stack symbolized) goes to gpurun_out.  Last in the session: an
+  # ASan CHECK exits 1, so the steps after it still run.
+  step build_sanitize_lib 600 make -s -C "$ROOT" -j16 sanitize-lib
+  for m in none malloc rccl; do
+    ASAN_OPTIONS="detect_leaks=0:log_path=$OUT/${TAG}_asan_teardown_$m" \
+      ASAN_SYMBOLIZER_PATH=/opt/rocm/lib/llvm/bin/llvm-symbolizer \
+      step asan_teardown_$m 120 "$ROOT/tools/asan_teardown" $m > "$OUT/${TAG}_asan_teardown_$m.out" 2>&1
+  done
+  P1_SAN_NORMAL_EXIT=1 ASAN_OPTIONS="detect_leaks=0:log_path=$OUT/${TAG}_san_stress_normal_exit" \
+    ASAN_SYMBOLIZER_PATH=/opt/rocm/lib/llvm/bin/llvm-symbolizer \
+    step san_stress_normal_exit 240 "$ROOT/tools/san/capi_san_stress" ${SAN_STRESS_S:-20} > "$OUT/${TAG}_san_stress_normal_exit.out" 2>&1
+fi
 cd /tmp && export TMPDIR=/tmp
 # kernel-trace stats and PMC passes per config (every k_scan launch of the
 # profiled command is a workload launch: --no-small-request)
