@@ -200,9 +200,15 @@ struct Runtime {
   p1hip_stats_t stats{};
 };
 
+// Never destroyed: the runtime state outlives every static destructor, so a
+// p1hip_* call made from a consumer's own atexit handler or static
+// destructor still finds a valid mutex and device list, and the library
+// issues no HIP call during process teardown (device memory is released
+// only by p1hip_shutdown; what a process leaves open, the driver reclaims
+// at exit).  The host containers it holds are reachable to the end.
 Runtime& rt() {
-  static Runtime r;
-  return r;
+  static Runtime* r = new Runtime();
+  return *r;
 }
 
 int dev_release(Dev& d) {
