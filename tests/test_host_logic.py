@@ -249,6 +249,24 @@ def test_capi_abi_version_and_comm_info_without_devices():
     assert ei.value.rc == -4
 
 
+def test_library_registers_no_exit_time_destructor():
+    """nothing of libp1hip.so runs at process exit that
+    could free device memory after the ROCm runtime is gone.  The runtime
+    singleton is never destroyed (p1hip.hip rt()), so the library registers
+    no process-exit destructor (__cxa_atexit); the only exit-time code left
+    is the thread_local error strings' (__cxa_thread_atexit, host memory)."""
+    import shutil
+
+    objdump = shutil.which("objdump")
+    if not objdump:
+        pytest.skip("binutils objdump not present")
+    import p1_amd
+
+    dis = subprocess.run([objdump, "-d", p1_amd.lib_path()], capture_output=True, text=True, check=True).stdout
+    calls = re.findall(r"call\s+\S+\s+<(__cxa_\w*atexit)@plt>", dis)
+    assert calls and set(calls) == {"__cxa_thread_atexit"}, sorted(set(calls))
+
+
 def test_capi_no_device_fails_loudly():
     """Without a GPU the product path raises; it never falls back to a CPU hash."""
     import p1_amd
