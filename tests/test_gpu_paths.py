@@ -411,3 +411,29 @@ def test_one_hardware_queue_per_process():
     assert n_null >= 1, "the runtime log format changed: no queue creation lines"
     assert len(q_miner) == 1 and len(q_lib) == 1
     assert len(q_null) == 2
+
+
+def test_config4_eight_logical_devices_on_one_gpu(reinit, large):
+    """The library-mode N = 8 shape of configs[3] on the one GPU a box has:
+    GPU 0 listed 8 times, 8 host threads, p1hip_plan_shards' 8 contiguous
+    cost-balanced shards of [0, 2^38), host combine (RCCL cannot pair a GPU
+    with itself, hence P1HIP_NO_RCCL; the 8-GPU run is the driver's).  The
+    answer is configs[3]'s pinned one, every shard is active and they tile
+    the range, and bench.py would refuse to time this shape as an 8-GPU run
+    (no communicator)."""
+    import bench
+
+    g = reinit((0,) * 8, P1HIP_NO_RCCL=1)
+    g.reset_stats()
+    want = large[(b"bradfitz", 0, (1 << 38) - 1)]
+    assert g.scan("bradfitz", 0, (1 << 38) - 1) == want
+    shards = [g.get_device_stats(i) for i in range(8)]
+    assert all(s["active"] for s in shards)
+    assert shards[0]["shard_first"] == 0 and shards[-1]["shard_last"] == (1 << 38) - 1
+    for a, b in zip(shards, shards[1:]):
+        assert b["shard_first"] == a["shard_last"] + 1
+    assert sum(s["scan_nonces"] for s in shards) == 1 << 38
+    assert [(s["shard_first"], s["shard_last"]) for s in shards] == \
+        g.plan_shards("bradfitz", 0, (1 << 38) - 1, 8)
+    with pytest.raises(bench.TopologyError):
+        bench.library_topology("library", 8, [g.comm_info(i) for i in range(8)])
