@@ -30,7 +30,15 @@ scan-kernel A/Bs in profiles/r01n_e64_ab.jsonl, profiles/r01r_loop_offset_sweep.
    4-byte instruction that breaks it: by widening the preceding 4-byte VALU
    (VOP1/VOP2/VOPC e32 -> e64, same operands) where possible, else by
    inserting one `s_nop 0` before the next 8-byte instruction.
-3. --drop-asm-nops: remove the `s_nop 0` LLVM's hazard recognizer puts after
+3. --ab-nop[=N]: one `s_nop N` (default 0) before every full-rate VALU op
+   that directly follows a half-rate one in a loop body (no scalar
+   instruction between them).  gfx950 issues two full-rate VALU ops of two
+   different waves in one 4-cycle slot (SQ_ACTIVE_INST_VALU2) but a
+   half-rate op alone; with the oldest wave issuing every slot, the waves
+   behind it rarely hold a full-rate op when it does, and a scalar filler
+   after the half-rate op hands the slot to them (tools/gen_dual.py:
+   A,nop,B pairs 93% of its B ops where A,B pairs 0-56%).  A/B option.
+4. --drop-asm-nops: remove the `s_nop 0` LLVM's hazard recognizer puts after
    an inline-asm block whose next instruction reads the block's result.  For
    inline asm it must assume a dst_sel (16-bit) forwarding hazard on gfx950;
    our blocks are single 32-bit v_bitop3_b32, which LLVM itself issues
@@ -180,6 +188,57 @@ def pass_align(lines, align, offset, stats):
     return out
 
 
+HALF_RATE = {"v_alignbit_b32", "v_add3_u32", "v_alignbyte_b32", "v_perm_b32", "v_xad_u32", "v_or3_b32",
+             "v_lshl_or_b32", "v_lshl_add_u32", "v_add_lshl_u32", "v_and_or_b32", "v_bfi_b32", "v_bfe_u32",
+             "v_mad_u32_u24", "v_pk_add_u16", "v_cndmask_b32_e64"}
+RE_SGPR_OP = re.compile(r"(^|[\s,])s(\d+|\[\d+:\d+\])\b")
+
+
+def issue_class(ins):
+    """'A' half-rate VALU (3-input VOP3 integer ops; a VOP3 op with an SGPR
+    source, tools/gen_dual.py kind k), 'B' full-rate VALU, 'S' anything else"""
+    op, _, ops = ins.partition(" ")
+    if not op.startswith("v_"):
+        return "S"
+    if op in HALF_RATE:
+        return "A"
+    srcs = ",".join(operands(ops)[1:])
+    if (op.endswith("_e64") or op.startswith("v_bitop3")) and RE_SGPR_OP.search(srcs):
+        return "A"
+    return "B"
+
+
+def loop_regions(lines):
+    regions = []
+    for h in loop_headers(lines):
+        label = RE_LABEL.match(lines[h]).group(1)
+        for j in range(h + 1, min(len(lines), h + 40000)):
+            m = RE_BRANCH.match(lines[j].strip())
+            if m and m.group(1) == label:
+                regions.append((h, j))
+                break
+    return regions
+
+
+def pass_ab_nop(lines, nop, stats):
+    inside = set()
+    for a, b in loop_regions(lines):
+        inside.update(range(a + 1, b + 1))
+    out, last = [], None
+    for i, ln in enumerate(lines):
+        s = ln.strip()
+        if i in inside and is_instr(s):
+            c = issue_class(s)
+            if c == "B" and last == "A":
+                out.append(f"\ts_nop {nop}")
+                stats["ab_nops"] += 1
+            last = c
+        elif RE_LABEL.match(s):
+            last = None
+        out.append(ln)
+    return out
+
+
 def pass_parity(lines, stats):
     """Loop bodies (label .. branch back to it) start at 4 mod 8 (pass_align
     with offset 4); keep every 8-byte instruction in them at 4 mod 8.  Loops
@@ -230,11 +289,14 @@ def main():
     src, dst = sys.argv[1], sys.argv[2]
     args = sys.argv[3:]
     opt = {a.split("=")[0]: (a.split("=")[1] if "=" in a else True) for a in args}
-    stats = {"e64_converted": 0, "asm_nops_dropped": 0, "loops_aligned": 0, "parity_widened": 0, "parity_nops": 0}
+    stats = {"e64_converted": 0, "asm_nops_dropped": 0, "loops_aligned": 0, "parity_widened": 0, "parity_nops": 0,
+             "ab_nops": 0}
     lines = open(src).read().split("\n")
     lines = pass_encode(lines, "--no-e64" not in opt, "--drop-asm-nops" in opt, stats)
     if "--align-loops" in opt:
         lines = pass_align(lines, int(opt["--align-loops"]), int(opt.get("--loop-offset", 0)), stats)
+    if "--ab-nop" in opt:
+        lines = pass_ab_nop(lines, 0 if opt["--ab-nop"] is True else int(opt["--ab-nop"]), stats)
     if "--loop-parity" in opt:
         if opt.get("--align-loops") != "3" or opt.get("--loop-offset") != "4":
             raise SystemExit("--loop-parity needs --align-loops=3 --loop-offset=4")
