@@ -220,16 +220,32 @@ def loop_regions(lines):
     return regions
 
 
-def pass_ab_nop(lines, nop, stats):
+def pass_ab_nop(lines, nop, stats, where="ab"):
+    """where: 'ab' = before a full-rate op after a half-rate one; 'abb' = the
+    same, only when the full-rate op starts a run of at least two; 'ba' =
+    before a half-rate op after a full-rate one"""
     inside = set()
     for a, b in loop_regions(lines):
         inside.update(range(a + 1, b + 1))
+    cls = {i: issue_class(lines[i].strip()) for i in inside if is_instr(lines[i].strip())}
+
+    def next_cls(i):
+        for j in range(i + 1, len(lines)):
+            if j in cls:
+                return cls[j]
+            if RE_LABEL.match(lines[j].strip()):
+                return None
+        return None
+
     out, last = [], None
     for i, ln in enumerate(lines):
         s = ln.strip()
-        if i in inside and is_instr(s):
-            c = issue_class(s)
-            if c == "B" and last == "A":
+        if i in cls:
+            c = cls[i]
+            hit = {"ab": c == "B" and last == "A",
+                   "abb": c == "B" and last == "A" and next_cls(i) == "B",
+                   "ba": c == "A" and last == "B"}[where]
+            if hit:
                 out.append(f"\ts_nop {nop}")
                 stats["ab_nops"] += 1
             last = c
@@ -296,7 +312,8 @@ def main():
     if "--align-loops" in opt:
         lines = pass_align(lines, int(opt["--align-loops"]), int(opt.get("--loop-offset", 0)), stats)
     if "--ab-nop" in opt:
-        lines = pass_ab_nop(lines, 0 if opt["--ab-nop"] is True else int(opt["--ab-nop"]), stats)
+        lines = pass_ab_nop(lines, 0 if opt["--ab-nop"] is True else int(opt["--ab-nop"]), stats,
+                            opt.get("--nop-where", "ab"))
     if "--loop-parity" in opt:
         if opt.get("--align-loops") != "3" or opt.get("--loop-offset") != "4":
             raise SystemExit("--loop-parity needs --align-loops=3 --loop-offset=4")
