@@ -111,6 +111,40 @@ def test_post_pass_assembles_with_parity(tmp_path):
     assert len(loop) == 5 and all(a % 8 == 4 for a, n, _ in loop if n == 2), addr
 
 
+def test_ab_nop_waits_before_full_rate_after_half_rate(tmp_path):
+    """--ab-nop=3: one s_nop 3 before each full-rate VALU op that directly
+    follows a half-rate one inside a loop, the 4 (mod 8) parity kept."""
+    src, dst, obj = tmp_path / "a.s", tmp_path / "b.s", tmp_path / "b.o"
+    src.write_text(SNIPPET)
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_post.py"), str(src), str(dst),
+                    "--align-loops=3", "--loop-offset=4", "--ab-nop=3", "--loop-parity"], check=True, capture_output=True)
+    body = [ln.strip() for ln in dst.read_text().split("\n")]
+    body = body[next(k for k, ln in enumerate(body) if ln.startswith(".LBB0_1:")):]
+    for i in (k for k, ln in enumerate(body) if ln.startswith("v_alignbit_b32")):
+        nxt = next(ln for ln in body[i + 1:] if ln.startswith("v_"))
+        assert body[i + 1] == "s_nop 3" and isa_post.issue_class(nxt) == "B", body
+    # add3 after the scalar s_add: no wait needed there, none inserted
+    j = next(k for k, ln in enumerate(body) if ln.startswith("v_add3_u32"))
+    assert not body[j - 1].startswith("s_nop 3")
+    subprocess.run([f"{LLVM}/llvm-mc", "-arch=amdgcn", "-mcpu=gfx950", "-filetype=obj", "-o", str(obj), str(dst)],
+                   check=True)
+    dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", str(obj)], capture_output=True, text=True,
+                         check=True).stdout
+    addr = [(int(m.group(2), 16), len(m.group(3).split()), m.group(1))
+            for m in re.finditer(r"^\s+(\w+).*//\s*([0-9A-F]+):\s*((?:[0-9A-F]{8}\s*)+)$", dis, re.M)]
+    assert all(a % 8 == 4 for a, n, op in addr if n == 2 and op.startswith("v_")), addr
+
+
+def test_issue_classes():
+    assert isa_post.issue_class("v_alignbit_b32 v1, v2, v2, 7") == "A"
+    assert isa_post.issue_class("v_add3_u32 v1, v2, v3, v4") == "A"
+    assert isa_post.issue_class("v_add_u32_e64 v42, s72, v35") == "A"  # VOP3 with an SGPR source (dual kind k)
+    assert isa_post.issue_class("v_add_u32_e64 v42, v7, v35") == "B"
+    assert isa_post.issue_class("v_bitop3_b32 v5, v1, v2, v3 bitop3:0x96") == "B"
+    assert isa_post.issue_class("v_add_u32_e32 v1, s5, v2") == "B"
+    assert isa_post.issue_class("s_nop 0") == "S"
+
+
 # ---------------------------------------------------------------------------
 # VERDICT r04 next #5: the roofline (0.649 on c4) sits at the floor of the
 # loop mix, so a toolchain or post-pass change that lengthens the per-nonce
@@ -177,6 +211,33 @@ def test_shipped_hot_loops_are_no_longer_than_pinned(shipped_loops):
     assert all(m["other"] == 0 for m in shipped_loops), [m for m in shipped_loops if m["other"]]
     # the post-pass parity rule holds inside every per-nonce loop
     assert all(m["n8_at_4_mod_8"] >= m["n8"] - 2 for m in shipped_loops)
+
+
+def test_shipped_hot_loops_wait_after_half_rate_runs(codeobj):
+    """Round 5: in every per-nonce loop a full-rate VALU op never follows a
+    half-rate one without the post-pass's s_nop 3 between them (the
+    dual-issue rule, DESIGN.md 4 "Dual issue"): losing it costs ~6%."""
+    import variant_report as vr
+
+    ins, inner, _ = vr.loops_of(codeobj)
+    checked = 0
+    for lo, hi in inner:
+        body = [t for a, sz, t in ins if lo <= a <= hi]
+        if sum(1 for t in body if t.startswith("v_")) <= 500:
+            continue
+        checked += 1
+        prev = None
+        for t in body:
+            c = isa_post.issue_class(t)
+            if c == "B" and prev == "A":
+                raise AssertionError(f"A->B without a wait in loop at {lo:#x}: {t}")
+            if c == "S":
+                prev = "S"
+                if t.startswith("s_nop 3"):
+                    continue
+            else:
+                prev = c
+    assert checked == 63, checked
 
 
 def test_k_scan_registers_keep_four_waves(codeobj):

@@ -49,6 +49,7 @@ Prints a one-line JSON summary of what changed to stderr.
 """
 import json
 import os
+sys_path_here = os.path.dirname(os.path.abspath(__file__))
 import re
 import subprocess
 import sys
@@ -220,10 +221,11 @@ def loop_regions(lines):
     return regions
 
 
-def pass_ab_nop(lines, nop, stats, where="ab"):
+def pass_ab_nop(lines, nop, stats, where="ab", table=None):
     """where: 'ab' = before a full-rate op after a half-rate one; 'abb' = the
     same, only when the full-rate op starts a run of at least two; 'ba' =
-    before a half-rate op after a full-rate one"""
+    before a half-rate op after a full-rate one.  table (ab only): the wait
+    by run lengths, {(A-run 1 or 2+, B-run 1 or 2+): N or -1 for none}."""
     inside = set()
     for a, b in loop_regions(lines):
         inside.update(range(a + 1, b + 1))
@@ -237,7 +239,7 @@ def pass_ab_nop(lines, nop, stats, where="ab"):
                 return None
         return None
 
-    out, last = [], None
+    out, last, arun = [], None, 0
     for i, ln in enumerate(lines):
         s = ln.strip()
         if i in cls:
@@ -245,12 +247,17 @@ def pass_ab_nop(lines, nop, stats, where="ab"):
             hit = {"ab": c == "B" and last == "A",
                    "abb": c == "B" and last == "A" and next_cls(i) == "B",
                    "ba": c == "A" and last == "B"}[where]
+            n = nop
+            if hit and table is not None:
+                n = table[(min(arun, 2), 2 if next_cls(i) == "B" else 1)]
+                hit = n >= 0
             if hit:
-                out.append(f"\ts_nop {nop}")
+                out.append(f"\ts_nop {n}")
                 stats["ab_nops"] += 1
+            arun = arun + 1 if (c == "A" and last == "A") else (1 if c == "A" else 0)
             last = c
         elif RE_LABEL.match(s):
-            last = None
+            last, arun = None, 0
         out.append(ln)
     return out
 
@@ -302,6 +309,7 @@ def pass_parity(lines, stats):
 
 
 def main():
+    sys.path.insert(0, sys_path_here)
     src, dst = sys.argv[1], sys.argv[2]
     args = sys.argv[3:]
     opt = {a.split("=")[0]: (a.split("=")[1] if "=" in a else True) for a in args}
@@ -311,9 +319,20 @@ def main():
     lines = pass_encode(lines, "--no-e64" not in opt, "--drop-asm-nops" in opt, stats)
     if "--align-loops" in opt:
         lines = pass_align(lines, int(opt["--align-loops"]), int(opt.get("--loop-offset", 0)), stats)
+    if "--pair-sched" in opt:
+        import pair_sched
+        stats.update(sched_segments=0, sched_moved=0)
+        lines = pair_sched.pass_pair_sched(lines, loop_regions(lines), is_instr, issue_class, stats,
+                                           3 if opt["--pair-sched"] is True else int(opt["--pair-sched"]))
     if "--ab-nop" in opt:
+        table = None
+        if "--ab-nop-table" in opt:  # N11,N12,N21,N22: (A-run 1|2+, B-run 1|2+)
+            v = [int(x) for x in opt["--ab-nop-table"].split(",")]
+            table = {(1, 1): v[0], (1, 2): v[1], (2, 1): v[2], (2, 2): v[3]}
         lines = pass_ab_nop(lines, 0 if opt["--ab-nop"] is True else int(opt["--ab-nop"]), stats,
-                            opt.get("--nop-where", "ab"))
+                            opt.get("--nop-where", "ab"), table)
+    if "--ba-nop" in opt:
+        lines = pass_ab_nop(lines, 0 if opt["--ba-nop"] is True else int(opt["--ba-nop"]), stats, "ba")
     if "--loop-parity" in opt:
         if opt.get("--align-loops") != "3" or opt.get("--loop-offset") != "4":
             raise SystemExit("--loop-parity needs --align-loops=3 --loop-offset=4")
