@@ -470,6 +470,15 @@ def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof
             ex["mix_issue_note"] = ("ideal SIMD cycles of the loop mix (A x 4.23 + B x 2.13, the fastest "
                                     "single-class issue costs measured by tools/valu_runs) / SIMD cycles spent "
                                     "per 64 nonces")
+            v2 = pmc.get("dual_valu_issue_quads_per_wave_instr")
+            if v2 is not None:
+                # DESIGN.md 4 "Dual issue": one VALU slot per 4 cycles, shared
+                # by two full-rate ops of different waves (SQ_ACTIVE_INST_VALU2)
+                b_share = mix_ab[1] / (mix_ab[0] + mix_ab[1])
+                ex["dual_issue"] = {"valu2_per_valu": v2, "full_rate_ops_paired": v2 / (b_share / 2),
+                                    "slot_model_simd_cycles_per_valu": 4.0 * (1.0 - v2),
+                                    "note": "SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU from the PMC summary; "
+                                            "full_rate_ops_paired = that / (full-rate share of the loop mix / 2)"}
         roof["executed"] = ex
     if cfg["b_tail"] != 1:
         # the algorithmic count charges both tail blocks per nonce; the kernel

@@ -262,6 +262,30 @@ def pass_ab_nop(lines, nop, stats, where="ab", table=None):
     return out
 
 
+def pass_prio(lines, prio_b, prio_a, stats):
+    """A/B option --prio=PB,PA: `s_setprio PB` before the first full-rate op
+    of every run and `s_setprio PA` before the first half-rate op of every
+    run inside the loop bodies (the issue arbiter prefers the higher
+    priority, then the older wave)."""
+    inside = set()
+    for a, b in loop_regions(lines):
+        inside.update(range(a + 1, b + 1))
+    out, last = [], None
+    for i, ln in enumerate(lines):
+        s = ln.strip()
+        if i in inside and is_instr(s):
+            c = issue_class(s)
+            if c in "AB" and c != last:
+                out.append(f"\ts_setprio {prio_b if c == 'B' else prio_a}")
+                stats["prio_switches"] = stats.get("prio_switches", 0) + 1
+            if c in "AB":
+                last = c
+        elif RE_LABEL.match(s):
+            last = None
+        out.append(ln)
+    return out
+
+
 def pass_parity(lines, stats):
     """Loop bodies (label .. branch back to it) start at 4 mod 8 (pass_align
     with offset 4); keep every 8-byte instruction in them at 4 mod 8.  Loops
@@ -331,6 +355,9 @@ def main():
             table = {(1, 1): v[0], (1, 2): v[1], (2, 1): v[2], (2, 2): v[3]}
         lines = pass_ab_nop(lines, 0 if opt["--ab-nop"] is True else int(opt["--ab-nop"]), stats,
                             opt.get("--nop-where", "ab"), table)
+    if "--prio" in opt:
+        pb, pa = (int(x) for x in opt["--prio"].split(","))
+        lines = pass_prio(lines, pb, pa, stats)
     if "--ba-nop" in opt:
         lines = pass_ab_nop(lines, 0 if opt["--ba-nop"] is True else int(opt["--ba-nop"]), stats, "ba")
     if "--loop-parity" in opt:
