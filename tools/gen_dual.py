@@ -44,6 +44,8 @@ KINDS = {
     "n": ("s_nop 0", False),
     "s": ("s_add_u32 s21, s21, 1", False),
     "N": ("s_nop 3", False),
+    "H": ("s_setprio 1", False),
+    "L": ("s_setprio 0", False),
 }
 
 SET1 = [
@@ -64,11 +66,19 @@ SET2 = [(p, (0, 4, 8, 12, 16, 20, 24, 28), (4,)) for p in ("aeee", "ae", "b", "a
        [(p, (0, 4), (2, 3, 4)) for p in ("ad", "ae", "aee", "aeee", "anb", "ama", "aMa", "asb", "aNb", "b", "d")] + \
        [(p, (4,), (4,)) for p in ("aMaM", "amam", "anbb", "anbbb", "aanbb", "aaanbb", "annb", "abnb", "anbnb", "asbsb",
                                    "adn", "and", "ansd", "aNbb", "aaNbb", "aaabb", "aaNbNb")]
+# round 3 (r05k): wave priorities.  Static: a wave's priority from its
+# block's slot on the CU (blocks b, b+CUs, b+2 CUs, b+3 CUs share a CU):
+# "/2" = half the waves at 1, "/4" = 0..3.  Dynamic: H / L tokens.
+SET3 = [(p, (4,), (4,)) for p in ("a", "b", "d", "ae", "aee", "ad", "aaee", "a/2", "b/2", "d/2", "ae/2", "aee/2",
+                                    "ad/2", "aaee/2", "a/4", "ae/4", "ad/4", "HaLe", "HaLee", "HaaLee", "HaLeee",
+                                    "HaaLe", "HaaaLee", "HaLd", "HaLdd", "LaHe", "HaHe", "HaaaLe", "HaaaaLe")]
 SET = os.environ.get("DUAL_SET", "1")
 if SET == "1":
     RUNS = [(p, (0, 4), (1, 4)) for p in SET1]
-else:
+elif SET == "2":
     RUNS = SET2
+else:
+    RUNS = SET3
 BODY_MIN = 240
 
 
@@ -85,7 +95,7 @@ def expand(pat):
 
 def body(pat):
     toks = expand(pat)
-    nchain = sum(1 for k, _ in toks if k not in "mMnsN")
+    nchain = sum(1 for k, _ in toks if k not in "mMnsNHL")
     reps = 1
     while len(toks) * reps < BODY_MIN or (nchain * reps) % NCH:
         reps += 1
@@ -98,10 +108,10 @@ def body(pat):
             lines.append(tmpl.format(d=d, s1=s1, s2=f"v{S2}", sink=SINK, rsink=SINK + r % 4))
             if k == "M":
                 r += 1
-            if k not in "mMnsN":
+            if k not in "mMnsNHL":
                 prev = d
                 v += 1
-    n_valu = sum(1 for k, _ in toks if k not in "nsN") * reps
+    n_valu = sum(1 for k, _ in toks if k not in "nsNHL") * reps
     return lines, n_valu
 
 
@@ -117,14 +127,22 @@ init = "\\n\\t".join([f"v_mov_b32 v{BASE + i}, %[s]" for i in range(NCH)] +
                       "s_mov_b32 s20, 12345", "s_mov_b32 s21, 0"])
 kernels = []
 for pat, aligns, wlist in RUNS:
+    pat, _, static = pat.partition("/")
     lines, nvalu = body(pat)
+    prio = ""
+    if static:
+        prio = (f"  const int slot = (int)(blockIdx.x / gridDim.x * 0 + blockIdx.x / (gridDim.x / {wlist[0]}));\n"
+                f"  if (slot % {static} == 1) __builtin_amdgcn_s_setprio(1);\n"
+                f"  if (slot % {static} == 2) __builtin_amdgcn_s_setprio(2);\n"
+                f"  if (slot % {static} == 3) __builtin_amdgcn_s_setprio(3);\n")
+        pat = pat + "/" + static
     for al in aligns:
         i = len(kernels)
         pre = ".p2align 6" + "\\n\\ts_nop 0" * (al // 4)
         asm = "\\n\\t".join(lines)
         out.append(f"""__global__ __launch_bounds__(256) void k{i}(uint64_t* out, uint32_t seed, int iters) {{
   asm volatile("{init}" : : [s] "v"(seed * (threadIdx.x + 1)) : {CLOB});
-  int cnt = iters;
+{prio}  int cnt = iters;
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   asm volatile("{pre}\\n1:\\n\\t{asm}\\n\\ts_sub_u32 %[c], %[c], 1\\n\\ts_cmp_lg_u32 %[c], 0\\n\\ts_cbranch_scc1 1b"
                : [c] "+s"(cnt) : : "scc", {CLOB});
