@@ -37,6 +37,7 @@ KINDS = {
     "k": ("v_add_u32_e64 {d}, s20, {d}", True),
     # full-rate, 4-byte VOP2
     "d": ("v_add_u32_e32 {d}, {s1}, {d}", True),
+    "D": ("v_add_u32_e32 {d}, s20, {d}", True),   # VOP2 with an SGPR source
     "y": ("v_xor_b32_e32 {d}, {s1}, {d}", True),
     "m": ("v_mov_b32_e32 v{sink}, {d}", True),   # reads a chain, writes a sink
     "M": ("v_mov_b32_e32 v{rsink}, {d}", True),  # reads a chain, writes one of 4 sinks in turn
@@ -72,13 +73,18 @@ SET2 = [(p, (0, 4, 8, 12, 16, 20, 24, 28), (4,)) for p in ("aeee", "ae", "b", "a
 SET3 = [(p, (4,), (4,)) for p in ("a", "b", "d", "ae", "aee", "ad", "aaee", "a/2", "b/2", "d/2", "ae/2", "aee/2",
                                     "ad/2", "aaee/2", "a/4", "ae/4", "ad/4", "HaLe", "HaLee", "HaaLee", "HaLeee",
                                     "HaaLe", "HaaaLee", "HaLd", "HaLdd", "LaHe", "HaHe", "HaaaLe", "HaaaaLe")]
+# round 4 (r05m): SGPR sources under per-run priorities
+SET4 = [(p, (4,), (4,)) for p in ("D", "k", "HaLD", "HaLk", "HkLe", "HcLe", "HaLDD", "HaLkk", "HkLD", "HaLb",
+                                    "HaLbb", "HaaLbb", "HaaLbbb", "HaaaLbbbb", "HaLee", "HcLd")]
 SET = os.environ.get("DUAL_SET", "1")
 if SET == "1":
     RUNS = [(p, (0, 4), (1, 4)) for p in SET1]
 elif SET == "2":
     RUNS = SET2
-else:
+elif SET == "3":
     RUNS = SET3
+else:
+    RUNS = SET4
 BODY_MIN = 240
 
 

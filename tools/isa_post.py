@@ -262,6 +262,49 @@ def pass_ab_nop(lines, nop, stats, where="ab", table=None):
     return out
 
 
+RE_ADD3 = re.compile(r"^v_add3_u32\s+(v\d+),\s*(v\d+),\s*(v\d+),\s*(v\d+)\s*$")
+
+
+def split_add3(ins):
+    """v_add3_u32 d, a, b, c (VGPR operands) -> two full-rate v_add_u32_e64,
+    the destination as the intermediate (read before it is overwritten)."""
+    m = RE_ADD3.match(ins.split(";")[0].strip())
+    if not m:
+        return None
+    d, a, b, c = m.groups()
+    for x, y, z in ((a, b, c), (a, c, b), (b, c, a)):
+        if d != z:
+            return [f"v_add_u32_e64 {d}, {x}, {y}", f"v_add_u32_e64 {d}, {d}, {z}"]
+    return None
+
+
+def pass_split_add3(lines, frac, stats):
+    """A/B option --split-add3=F: in each innermost loop, split F x (A - B)/3
+    of its VGPR-only v_add3_u32 (evenly spread) into two full-rate adds, so
+    that half-rate and full-rate ops balance (one of each per issue slot,
+    DESIGN.md 4 "Dual issue")."""
+    regions = loop_regions(lines)
+    inner = [r for r in regions if not any(o != r and r[0] < o[0] and o[1] < r[1] for o in regions)]
+    todo = set()
+    for a, b in inner:
+        idx = [k for k in range(a + 1, b + 1) if is_instr(lines[k].strip())]
+        cls = [issue_class(lines[k].strip()) for k in idx]
+        na, nb = cls.count("A"), cls.count("B")
+        cand = [k for k in idx if split_add3(lines[k].strip())]
+        budget = min(len(cand), max(0, int(round(frac * (na - nb) / 3.0))))
+        if budget:
+            step = len(cand) / budget
+            todo.update(cand[int(i * step)] for i in range(budget))
+    out = []
+    for i, ln in enumerate(lines):
+        if i in todo:
+            out += ["\t" + x for x in split_add3(ln.strip())]
+            stats["add3_split"] = stats.get("add3_split", 0) + 1
+        else:
+            out.append(ln)
+    return out
+
+
 def pass_prio(lines, prio_b, prio_a, stats):
     """A/B option --prio=PB,PA: `s_setprio PB` before the first full-rate op
     of every run and `s_setprio PA` before the first half-rate op of every
@@ -343,6 +386,8 @@ def main():
     lines = pass_encode(lines, "--no-e64" not in opt, "--drop-asm-nops" in opt, stats)
     if "--align-loops" in opt:
         lines = pass_align(lines, int(opt["--align-loops"]), int(opt.get("--loop-offset", 0)), stats)
+    if "--split-add3" in opt:
+        lines = pass_split_add3(lines, float(opt["--split-add3"]), stats)
     if "--pair-sched" in opt:
         import pair_sched
         stats.update(sched_segments=0, sched_moved=0)
