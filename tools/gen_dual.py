@@ -76,6 +76,9 @@ SET3 = [(p, (4,), (4,)) for p in ("a", "b", "d", "ae", "aee", "ad", "aaee", "a/2
 # round 4 (r05m): SGPR sources under per-run priorities
 SET4 = [(p, (4,), (4,)) for p in ("D", "k", "HaLD", "HaLk", "HkLe", "HcLe", "HaLDD", "HaLkk", "HkLD", "HaLb",
                                     "HaLbb", "HaaLbb", "HaaLbbb", "HaaaLbbbb", "HaLee", "HcLd")]
+# round 5 (r05q): can a half-rate op be the second of a slot?  Loop-like A:B mixes
+SET5 = [(p, (4,), (4,)) for p in ("HaLa", "HaLc", "HcLa", "HaaLaa", "HaLaa", "HaaLb", "HaaLbHaLbb", "HaaLbHaaLbHaLbb",
+                                    "HaaaLbb", "HaaaaLbbb", "HaaaaaaaLbbbbb", "HaLbHaaLb", "HaaLa", "LaHa")]
 SET = os.environ.get("DUAL_SET", "1")
 if SET == "1":
     RUNS = [(p, (0, 4), (1, 4)) for p in SET1]
@@ -83,8 +86,10 @@ elif SET == "2":
     RUNS = SET2
 elif SET == "3":
     RUNS = SET3
-else:
+elif SET == "4":
     RUNS = SET4
+else:
+    RUNS = SET5
 BODY_MIN = 240
 
 
