@@ -76,7 +76,7 @@ def deps(items):
     return preds
 
 
-def schedule(seg, cls_of, run=3):
+def schedule(seg, cls_of, run=3, amax=0):
     """seg: instruction strings of one segment (all movable).  Returns a new
     order (list of indices): ready full-rate ops are emitted in runs of up
     to `run`, half-rate ops between runs, critical path first within a
@@ -100,13 +100,15 @@ def schedule(seg, cls_of, run=3):
         cand = [i for i in ready if cls[i] == c]
         return max(cand, key=lambda i: (height[i], -i)) if cand else None
 
-    cur = None
+    cur, arun = None, 0
     while ready:
         i = pick("S")
         if i is None:
             b, a = pick("B"), pick("A")
             if run == 0:  # class-sticky: switch class only when the current one has nothing ready
-                if cur == "A":
+                if cur == "A" and amax and arun >= amax and b is not None:
+                    i = b  # cap the half-rate run
+                elif cur == "A":
                     i = a if a is not None else b
                 else:
                     i = b if b is not None else a
@@ -116,6 +118,7 @@ def schedule(seg, cls_of, run=3):
                 i = a
             else:
                 i = b
+            arun = arun + 1 if (cls[i] == "A" and cur == "A") else (1 if cls[i] == "A" else 0)
             cur = cls[i]
         ready.discard(i)
         order.append(i)
@@ -131,7 +134,7 @@ def schedule(seg, cls_of, run=3):
     return order
 
 
-def pass_pair_sched(lines, regions, is_instr, cls_of, stats, run=3):
+def pass_pair_sched(lines, regions, is_instr, cls_of, stats, run=3, amax=0):
     """Reorder the movable segments of every loop region in `lines`."""
     out = list(lines)
     done = set()
@@ -152,7 +155,7 @@ def pass_pair_sched(lines, regions, is_instr, cls_of, stats, run=3):
             done.update(seg_idx)
             if len(seg_idx) > 2:
                 seg = [out[i].strip() for i in seg_idx]
-                order = schedule(seg, cls_of, run)
+                order = schedule(seg, cls_of, run, amax)
                 moved = sum(1 for x, y in enumerate(order) if x != y)
                 if moved:
                     stats["sched_segments"] += 1
