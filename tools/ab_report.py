@@ -31,7 +31,7 @@ def main():
     rows = []
     for n in names:
         r = {"build": n}
-        for cfg in ("c2", "c4"):
+        for cfg in ("c2", "c3", "c4"):
             b = bench_line(os.path.join(out_dir, f"{tag}_{n}_{cfg}.json"))
             if b:
                 r[cfg] = {"GH_s": b["value"], "frac": b["roofline"].get("frac"),

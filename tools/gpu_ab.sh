@@ -15,6 +15,9 @@ run() {  # run <name> <lib>
   local name=$1 lib=$2
   echo "== $name ($(date +%T))"
   P1HIP_LIB="$lib" timeout -k 10 300 python "$ROOT/bench.py" --config c2 --steps $C2STEPS --warmup 2 --no-cpu --no-by-config --no-small-request > "$OUT/${TAG}_${name}_c2.json" 2> "$OUT/${TAG}_${name}_c2.err" || return $?
+  if [ "${C3STEPS:-0}" != 0 ]; then
+    P1HIP_LIB="$lib" timeout -k 10 300 python "$ROOT/bench.py" --config c3 --steps $C3STEPS --warmup 1 --no-cpu --no-by-config --no-small-request > "$OUT/${TAG}_${name}_c3.json" 2> "$OUT/${TAG}_${name}_c3.err" || return $?
+  fi
   if [ "$C4STEPS" != 0 ]; then
     P1HIP_LIB="$lib" timeout -k 10 300 python "$ROOT/bench.py" --config c4 --steps $C4STEPS --warmup 1 --no-cpu --no-by-config --no-small-request > "$OUT/${TAG}_${name}_c4.json" 2> "$OUT/${TAG}_${name}_c4.err" || return $?
   fi
