@@ -478,13 +478,16 @@ def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof
                                     "cycles spent per 64 nonces")
             v2 = pmc.get("dual_valu_issue_quads_per_wave_instr")
             if v2 is not None:
-                # DESIGN.md 4 "Dual issue": one VALU slot per 4 cycles, shared
-                # by two full-rate ops of different waves (SQ_ACTIVE_INST_VALU2)
-                b_share = mix_ab[1] / (mix_ab[0] + mix_ab[1])
-                ex["dual_issue"] = {"valu2_per_valu": v2, "full_rate_ops_paired": v2 / (b_share / 2),
+                # DESIGN.md 4 "Dual issue": one VALU slot per 4 cycles; its
+                # first op of any class, a second full-rate op of another
+                # wave beside it (SQ_ACTIVE_INST_VALU2)
+                n_ab = mix_ab[0] + mix_ab[1]
+                ex["dual_issue"] = {"valu2_per_valu": v2, "valu_ops_in_shared_slots": 2.0 * v2,
+                                    "shared_slot_bound": 2.0 * min(mix_ab[1], n_ab / 2.0) / n_ab,
                                     "slot_model_simd_cycles_per_valu": 4.0 * (1.0 - v2),
-                                    "note": "SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU from the PMC summary; "
-                                            "full_rate_ops_paired = that / (full-rate share of the loop mix / 2)"}
+                                    "note": "SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU from the PMC summary; a slot holds "
+                                            "one op of any class first and a full-rate op of another wave second, "
+                                            "so at most 2 x min(B, (A+B)/2) / (A+B) of the ops can share a slot"}
         roof["executed"] = ex
     if cfg["b_tail"] != 1:
         # the algorithmic count charges both tail blocks per nonce; the kernel
