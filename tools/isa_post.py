@@ -393,7 +393,7 @@ def main():
         stats.update(sched_segments=0, sched_moved=0)
         lines = pair_sched.pass_pair_sched(lines, loop_regions(lines), is_instr, issue_class, stats,
                                            3 if opt["--pair-sched"] is True else int(opt["--pair-sched"]),
-                                           int(opt.get("--sched-amax", 0)))
+                                           int(opt.get("--sched-amax", 0)), int(opt.get("--sched-bmax", 0)))
     if "--ab-nop" in opt:
         table = None
         if "--ab-nop-table" in opt:  # N11,N12,N21,N22: (A-run 1|2+, B-run 1|2+)

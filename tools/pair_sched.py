@@ -76,7 +76,7 @@ def deps(items):
     return preds
 
 
-def schedule(seg, cls_of, run=3, amax=0):
+def schedule(seg, cls_of, run=3, amax=0, bmax=0):
     """seg: instruction strings of one segment (all movable).  Returns a new
     order (list of indices): ready full-rate ops are emitted in runs of up
     to `run`, half-rate ops between runs, critical path first within a
@@ -108,6 +108,8 @@ def schedule(seg, cls_of, run=3, amax=0):
             if run == 0:  # class-sticky: switch class only when the current one has nothing ready
                 if cur == "A" and amax and arun >= amax and b is not None:
                     i = b  # cap the half-rate run
+                elif cur == "B" and bmax and brun >= bmax and a is not None:
+                    i = a  # cap the full-rate run
                 elif cur == "A":
                     i = a if a is not None else b
                 else:
@@ -134,7 +136,7 @@ def schedule(seg, cls_of, run=3, amax=0):
     return order
 
 
-def pass_pair_sched(lines, regions, is_instr, cls_of, stats, run=3, amax=0):
+def pass_pair_sched(lines, regions, is_instr, cls_of, stats, run=3, amax=0, bmax=0):
     """Reorder the movable segments of every loop region in `lines`."""
     out = list(lines)
     done = set()
@@ -155,7 +157,7 @@ def pass_pair_sched(lines, regions, is_instr, cls_of, stats, run=3, amax=0):
             done.update(seg_idx)
             if len(seg_idx) > 2:
                 seg = [out[i].strip() for i in seg_idx]
-                order = schedule(seg, cls_of, run, amax)
+                order = schedule(seg, cls_of, run, amax, bmax)
                 moved = sum(1 for x, y in enumerate(order) if x != y)
                 if moved:
                     stats["sched_segments"] += 1
