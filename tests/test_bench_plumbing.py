@@ -135,6 +135,24 @@ def test_roofline_assembly_c4_fractions_below_one():
         assert "frac" not in mix and mix["speed_vs_unhoisted_mix"] > 1.0
 
 
+def test_roofline_assembly_round5_c4_dual_issue_fields():
+    """The r05t c4 run (2^38 nonces in 5.215 s, PMC VALU2 0.385): frac 0.928,
+    the slot-bound mix fraction below 1, and the shared-slot share below its
+    bound (a slot pairs any first op with a full-rate second)."""
+    cfg = bench.CONFIGS["c4"]
+    pmc = {"valu_wave_instr_per_nonce": 1186.3, "effective_clock_GHz": 2.375, "hbm_bytes_per_launch": 1.6e6,
+           "dual_valu_issue_quads_per_wave_instr": 0.385}
+    roof = bench.assemble_roofline("c4", cfg, _stats(1 << 38, 5215.1), 1, pmc, "x", (5.214e9, "y"))
+    assert 0.92 < roof["frac"] < 0.94
+    ex = roof["executed"]
+    if "mix_issue_frac" in ex:  # needs the committed variant reports
+        assert 0.85 < ex["mix_issue_frac"] < 1.0
+        d = ex["dual_issue"]
+        assert abs(d["valu_ops_in_shared_slots"] - 0.77) < 1e-9
+        assert d["valu_ops_in_shared_slots"] <= d["shared_slot_bound"] <= 1.0
+        assert abs(d["slot_model_simd_cycles_per_valu"] - 4 * (1 - 0.385)) < 1e-9
+
+
 def test_roofline_assembly_rejects_frac_above_one():
     # the same 2^38 nonces "in" 2 s would be 1.9x the peak: refused, not printed
     cfg = bench.CONFIGS["c4"]
