@@ -48,13 +48,20 @@ def test_code_object_is_gfx950_with_all_kernels(codeobj):
         assert f"{k}.kd" in hdr
 
 
-def test_hot_loops_keep_4_mod_8_parity(codeobj):
+def test_shipped_build_uses_priorities_not_parity(codeobj):
+    """Round 5: under per-run wave priorities the 4 (mod 8) parity rule of
+    r01 no longer pays (r05aa A/B: its s_nops cost 0.3-1%), so the shipped
+    post-pass runs the schedule and the priorities without it; the parity
+    pass stays an option (DESIGN.md 4 "Dual issue")."""
+    mk = open(os.path.join(ROOT, "Makefile")).read()
+    line = next(ln for ln in mk.split("\n") if ln.startswith("ISAPOST ?="))
+    assert "--pair-sched=0" in line and "--prio=0,1" in line and "--loop-parity" not in line, line
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_parity.py"), codeobj],
                        capture_output=True, text=True, check=True)
     import json
 
     d = json.loads(r.stdout)
-    assert d["loops"] >= 32 and d["frac"] > 0.99, d
+    assert d["loops"] >= 32, d
 
 
 def test_scan_loops_are_vop3_only(codeobj):
@@ -230,8 +237,6 @@ def test_shipped_hot_loops_are_no_longer_than_pinned(shipped_loops):
         assert near, (v, (a, b), sorted(sigs))
         assert min(x + y for x, y in near) <= a + b + LOOP_TOL, (v, near)
     assert all(m["other"] == 0 for m in shipped_loops), [m for m in shipped_loops if m["other"]]
-    # the post-pass parity rule holds inside every per-nonce loop
-    assert all(m["n8_at_4_mod_8"] >= m["n8"] - 2 for m in shipped_loops)
 
 
 def test_shipped_hot_loops_switch_priority_per_run(codeobj):
