@@ -17,7 +17,7 @@ DEVHDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/fast_variants.in
 # leaves short still fits after the growth; the long ones it expands are the
 # variant dispatch's, outside every loop.
 DEVFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) --cuda-device-only -Wall -mllvm -amdgpu-s-branch-bits=15 $(DEVEXTRA)
-ISAPOST ?= --align-loops=3 --loop-offset=4 --pair-sched=0 --sched-amax=5 --sched-bmax=4 --prio=0,1
+ISAPOST ?= --no-e64 --align-loops=3 --loop-offset=4 --pair-sched=0 --sched-amax=5 --sched-bmax=4 --prio=0,1
 BUILD := build
 
 all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios \

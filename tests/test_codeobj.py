@@ -56,6 +56,7 @@ def test_shipped_build_uses_priorities_not_parity(codeobj):
     mk = open(os.path.join(ROOT, "Makefile")).read()
     line = next(ln for ln in mk.split("\n") if ln.startswith("ISAPOST ?="))
     assert "--pair-sched=0" in line and "--prio=0,1" in line and "--loop-parity" not in line, line
+    assert "--no-e64" in line, line
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_parity.py"), codeobj],
                        capture_output=True, text=True, check=True)
     import json
@@ -64,13 +65,15 @@ def test_shipped_build_uses_priorities_not_parity(codeobj):
     assert d["loops"] >= 32, d
 
 
-def test_scan_loops_are_vop3_only(codeobj):
-    """Inside the loops no full-rate op is left in its 4-byte VOP2 form."""
+def test_scan_loops_keep_compiler_encodings(codeobj):
+    """Round 5 (r05ad A/B: c3 +2.9%, c4 +0.3%): under per-run priorities the
+    post-pass no longer widens full-rate VOP2 ops to VOP3 (r01's reason, the
+    4 (mod 8) parity, is retired), so LLVM's 4-byte forms ship."""
     dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", codeobj], capture_output=True, text=True,
                          check=True).stdout
     n_e32 = len(re.findall(r"\bv_(add_u32|lshrrev_b32|xor_b32)_e32\b", dis))
     n_e64 = len(re.findall(r"\bv_(add_u32|lshrrev_b32|xor_b32)_e64\b", dis))
-    assert n_e64 > 10000 and n_e32 < n_e64 // 50, (n_e32, n_e64)
+    assert n_e32 > 10000 and n_e64 < n_e32, (n_e32, n_e64)
 
 
 def test_widen_and_convertible():

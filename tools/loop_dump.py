@@ -21,7 +21,7 @@ def main():
     ap.add_argument("mode", type=int)
     ap.add_argument("trail", choices=["true", "false"])
     ap.add_argument("out")
-    ap.add_argument("--isapost", default="--align-loops=3 --loop-offset=4 --pair-sched=0 --sched-amax=5 --sched-bmax=4 --prio=0,1")
+    ap.add_argument("--isapost", default="--no-e64 --align-loops=3 --loop-offset=4 --pair-sched=0 --sched-amax=5 --sched-bmax=4 --prio=0,1")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as td:
         inc = os.path.join(td, "v.inc")

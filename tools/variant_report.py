@@ -182,7 +182,7 @@ def main():
     ap.add_argument("--jobs", type=int, default=8)
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--waves", type=int, default=0)
-    ap.add_argument("--isapost", default="--align-loops=3 --loop-offset=4 --pair-sched=0 --sched-amax=5 --sched-bmax=4 --prio=0,1")
+    ap.add_argument("--isapost", default="--no-e64 --align-loops=3 --loop-offset=4 --pair-sched=0 --sched-amax=5 --sched-bmax=4 --prio=0,1")
     a = ap.parse_args()
     if a.explain is not None:
         head, rows = explain(a.explain or [os.path.join(ROOT, "profiles/r03f_variant_report.jsonl")])
