@@ -8,20 +8,26 @@ HDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/planner.hpp $(CSRC)
         $(CSRC)/scan_abi.hpp include/p1hip.h
 # what the device code includes (the host-side planner does not rebuild it)
 DEVHDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/fast_variants.inc $(CSRC)/scan_abi.hpp
-# device code: HIP C++ -> gfx950 assembly -> tools/isa_post.py peephole
-# (VOP2 -> VOP3 encodings of full-rate integer ops, every inner loop started
-# at 4 mod 8 bytes; see DESIGN.md "Build") -> assembled + linked code object,
-# embedded in libp1hip.so.  The post-pass widens ~32k 4-byte instructions to
-# 8 bytes after the compiler has relaxed its branches, so the compiler is told
-# that branches reach only half their real range (+-2^15 dwords): a branch it
-# leaves short still fits after the growth; the long ones it expands are the
-# variant dispatch's, outside every loop.
+# device code: HIP C++ -> gfx950 assembly -> tools/isa_post.py post-pass
+# (ISAPOST: LLVM's own encodings kept (--no-e64); loop labels aligned; every
+# loop body's straight-line segments reordered into runs of one issue class
+# (tools/pair_sched.py) with `s_setprio 1` / `s_setprio 0` before each
+# half-rate / full-rate run; DESIGN.md 4 "Dual issue") -> assembled + linked
+# code object, embedded in libp1hip.so.
+# -amdgpu-s-branch-bits=15: the post-pass inserts ~21.7k 4-byte s_setprio and
+# the loop-alignment padding AFTER the compiler has relaxed its branches, so
+# the compiler is told branches reach half their real range (+-2^14 of
+# +-2^15 dwords) and a branch it leaves short still fits after the growth
+# (shipped object: largest displacement 15,551 dwords; the long branches it
+# expands are the variant dispatch's, outside every per-nonce loop).  A
+# branch that did not fit would fail the assembly ("branch size exceeds
+# simm16"), never build wrong code (tests/test_codeobj.py).
 DEVFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) --cuda-device-only -Wall -mllvm -amdgpu-s-branch-bits=15 $(DEVEXTRA)
 ISAPOST ?= --no-e64 --align-loops=3 --loop-offset=4 --pair-sched=0 --sched-amax=5 --sched-bmax=4 --prio=0,1
 BUILD := build
 
 all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios \
-     tools/lsp_fake_miner tools/queue_ctl tools/wcal tools/vbank
+     tools/lsp_fake_miner tools/queue_ctl tools/wcal tools/vbank tools/libp1clock.so
 
 # The assembly and object stages are intermediates: once the code object
 # exists, a tree without them (the GPU box's copy leaves the 16 MB of .s out,
@@ -31,7 +37,7 @@ $(BUILD)/p1hip_kernels.s: $(CSRC)/p1hip_kernels.hip $(DEVHDRS) Makefile
 	mkdir -p $(BUILD)
 	$(HIPCC) $(DEVFLAGS) -S -o $@ $(CSRC)/p1hip_kernels.hip
 
-$(BUILD)/p1hip_kernels.post.s: $(BUILD)/p1hip_kernels.s tools/isa_post.py
+$(BUILD)/p1hip_kernels.post.s: $(BUILD)/p1hip_kernels.s tools/isa_post.py tools/pair_sched.py
 	python3 tools/isa_post.py $< $@ $(ISAPOST)
 
 $(BUILD)/p1hip_kernels.o: $(BUILD)/p1hip_kernels.post.s
@@ -83,6 +89,11 @@ tools/queue_ctl: tools/queue_ctl.cpp include/p1hip.h p1_amd/libp1hip.so
 # measurement program: WRITE_SIZE/FETCH_SIZE calibration for k_scan's partials
 tools/wcal: tools/wcal.hip
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -o $@ tools/wcal.hip
+
+# measurement library: shader-clock stamps around bench.py's timed steps
+# (not linked into anything; bench.py loads it with ctypes)
+tools/libp1clock.so: tools/clock_probe.hip
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared --offload-arch=$(ARCH) -Wall -o $@ tools/clock_probe.hip
 
 # measurement program: VALU issue cost vs operand VGPR banks
 tools/vbank: tools/vbank.hip
@@ -198,7 +209,7 @@ isa: $(BUILD)/p1hip_kernels.post.s
 	$(HIPCC) $(DEVFLAGS) -c -o /dev/null $(CSRC)/p1hip_kernels.hip -Rpass-analysis=kernel-resource-usage 2> $(BUILD)/resource.txt || true
 
 clean:
-	rm -f p1_amd/libp1hip.so tools/queue_ctl tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios tools/lsp_fake_miner tools/wcal tools/vbank
+	rm -f p1_amd/libp1hip.so tools/libp1clock.so tools/queue_ctl tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios tools/lsp_fake_miner tools/wcal tools/vbank
 	rm -rf $(BUILD)/p1hip_kernels* $(BUILD)/p1hip_host.o
 	$(MAKE) -C oracle clean
 .PHONY: all oracle clean isa variant sanitize sanitize-emu sanitize-lib sanitize-lib-tsan fuzz

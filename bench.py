@@ -37,6 +37,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 import time
@@ -75,14 +76,14 @@ GOLDEN = os.path.join(ROOT, "tests", "golden", "golden.json")
 ALG_MIX = {"v_alignbit_b32": 576, "v_bitop3_b32": 352, "v_add3_u32": 240, "v_add_u32": 120,
            "v_lshrrev_b32": 96}
 VALU_PEAK_PROFILE = "profiles/r01_valu_peak.jsonl"
-# Per-variant loop mix of the shipped kernel (tools/variant_report.py; later
-# files add variants): A "half-rate" ops (v_alignbit_b32, v_add3_u32, ...)
+# Per-variant loop mix of the shipped kernel (tools/variant_report.py run
+# through the shipped post-pass in round 6: all 78 variants, VALU counts
+# identical to the r02d/r02k/r03f reports): A "half-rate" ops (v_alignbit_b32, v_add3_u32, ...)
 # and B full-rate ops per nonce.  A SIMD issues VALU ops in 4-cycle slots; an
 # A op only as the first op of a slot, a B op also as the second (another
 # wave's), so a loop cannot issue in fewer than 4 x max(A, (A + B) / 2)
 # SIMD cycles per 64 nonces (DESIGN.md 4 "Dual issue", tools/gen_dual.py).
-VARIANT_PROFILES = ["profiles/r02d_variant_report.jsonl", "profiles/r02k_variant_report_mode5.jsonl",
-                    "profiles/r03f_variant_report.jsonl"]
+VARIANT_PROFILES = ["profiles/r06_variant_report.jsonl"]
 VARIANT_PROFILE = ", ".join(VARIANT_PROFILES)
 SLOT_CYCLES = 4.0  # SIMD cycles per VALU issue slot (gfx950; DESIGN.md 4 "Dual issue")
 
@@ -120,6 +121,27 @@ def job_total(cfg, n):
     return cfg["total"] if "total" in cfg else cfg["per_gpu"] * n
 
 
+def layout_config(spec):
+    """--layout L,START[,N]: a measurement job outside BASELINE's configs --
+    tools/sweep.py's L-byte message, nonces [START, START + N) (N default
+    2^32) -- to profile one tail layout (the two-block
+    TRAIL loops).  Same kernel path as every scan; no pinned answer."""
+    parts = [int(x, 0) for x in spec.split(",")]
+    if len(parts) not in (2, 3) or parts[0] < 0 or parts[1] < 0:
+        raise UsageError(f"bench.py: --layout L,START[,N], got {spec!r}")
+    L, start = parts[0], parts[1]
+    n = parts[2] if len(parts) == 3 else 1 << 32
+    d = len(str(start))
+    if len(str(start + n - 1)) != d:
+        raise UsageError("bench.py: --layout range must stay inside one decade (one kernel variant)")
+    b_tail = 1 if (L + 1) % 64 + d + 9 <= 64 else 2
+    msg = bytes((33 + (i * 7) % 90) for i in range(L))
+    return {"msg": msg, "total": n, "lo": start, "hi": start + n - 1, "b_tail": b_tail, "layout": [L, d],
+            "variant": list(fast_variant(L, d)),
+            "desc": f"layout L={L} d={d} (tools/sweep.py message, variant {list(fast_variant(L, d))}), "
+                    f"nonces [{start}, {start + n}) on each run"}
+
+
 def known_answer(cfg, n):
     """The exact answer of this job when one is pinned independently of the
     GPU: tests/golden/golden.json's large vectors (configs[1]: the survey's
@@ -131,6 +153,8 @@ def known_answer(cfg, n):
         with open(GOLDEN) as f:
             vecs = json.load(f)["scan"]
     except (OSError, ValueError, KeyError):
+        return None, None
+    if "lo" in cfg:
         return None, None
     for v in vecs:
         if v.get("large") and bytes.fromhex(v["msg_hex"]) == cfg["msg"] and v["lower"] == 0 \
@@ -225,17 +249,30 @@ def workload_mix(msg_len, lo, hi):
     return (a / w, b / w) if w else None
 
 
-def pmc_summary(config):
-    """Newest committed rocprofv3 PMC summary of this config's k_scan launch
-    (profiles/*_pmc_summary.json written by tools/summarize_prof.py; the
-    counters come from separate --pmc passes of the same bench command)."""
+def profile_tag_key(path):
+    """Session order of a profiles/ file: round number, then the session
+    letters by length and then alphabet (r05z < r05aa < r05ag), so "newest"
+    is not an accident of lexical sorting (VERDICT r05 weak #2)."""
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+
+def pmc_summary(config, codeobj):
+    """The committed rocprofv3 PMC summary of this config's k_scan launches
+    that was taken on THIS code object: profiles/*_pmc_summary.json written
+    by tools/summarize_prof.py carry the codeobj_sha256 of the library the
+    profiled command loaded (the counters come from separate --pmc passes of
+    the same bench command).  Newest session among the matches; (None,
+    None) when no summary was taken on this build."""
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
+    for p in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")):
         with open(p) as f:
             d = json.load(f)
-        if d.get("config", "c2") == config:
-            best = (d, os.path.relpath(p, ROOT))
-    return best if best else (None, None)
+        if d.get("config", "c2") != config or not codeobj or d.get("codeobj_sha256") != codeobj:
+            continue
+        if best is None or profile_tag_key(p) > profile_tag_key(best[1]):
+            best = (d, p)
+    return (best[0], os.path.relpath(best[1], ROOT)) if best else (None, None)
 
 
 def host_cores():
@@ -343,19 +380,24 @@ def scaling_report(units, steps, ms_per_step):
     return rep
 
 
-def rocprof_row(config):
-    """Newest committed rocprofv3 summary of this config's timed k_scan
-    launches (profiles/*_<config>_kernel_stats_workload.csv, the row over the
-    launches after the warm-up ones, tools/summarize_prof.py --skip-launches):
+def rocprof_row(config, codeobj):
+    """The committed rocprofv3 summary of this config's timed k_scan
+    launches taken on THIS code object (profiles/*_<config>_kernel_stats_
+    workload.csv, the row over the launches after the warm-up ones,
+    tools/summarize_prof.py --skip-launches; its Codeobj_SHA256 column names
+    the code object the profiled command ran).  Newest matching session:
     (average ns per launch, source) or (None, None)."""
     import csv
 
-    best = (None, None)
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_kernel_stats_workload.csv"))):
+    best, key = (None, None), None
+    for p in glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_kernel_stats_workload.csv")):
         with open(p) as f:
             for row in csv.DictReader(f):
-                if row["Name"].startswith("k_scan (launches after"):
-                    best = (float(row["AverageNs"]), os.path.relpath(p, ROOT))
+                if not (row["Name"].startswith("k_scan (launches after") and codeobj
+                        and row.get("Codeobj_SHA256") == codeobj):
+                    continue
+                if key is None or profile_tag_key(p) > key:
+                    best, key = (float(row["AverageNs"]), os.path.relpath(p, ROOT)), profile_tag_key(p)
     return best
 
 
@@ -363,58 +405,140 @@ class RooflineError(ValueError):
     pass
 
 
-# fractions that are not measured by this run (frac_rocprof divides by the
-# newest COMMITTED rocprofv3 average, possibly of an older build): a value
-# above 1 there says the committed profile is stale, not that this run's
-# timing is wrong, so it is reported beside the line instead of refusing it
-NOT_THIS_RUN_FRACS = ("frac_rocprof",)
-
-
-def check_fracs(roof, b_tail):
-    """No field named frac / frac_* computed from this run's own measurements
-    may exceed 1 for a 1-block config: a fraction of the peak above 1 would
-    say the timed kernel is not doing the work it is charged with (VERDICT r03
-    weak #3).  Raises RooflineError.  A committed-profile fraction above 1
-    (NOT_THIS_RUN_FRACS) is moved to `stale_profile` instead."""
-    if b_tail != 1:
-        return
-    for k in NOT_THIS_RUN_FRACS:
-        v = roof.get(k)
+def check_work_bound(roof):
+    """Refuse a line whose kernel could not have done the work it is charged
+    with.  The algorithmic `frac` is a speed ratio,
+    not a utilisation: the kernel hoists rounds 0..FV-1 and the constant
+    schedule words, so a fast layout legitimately exceeds 1 (the r05af
+    sweep's [13,6] layouts: 1.052).  The bound is on instructions the kernel
+    must execute instead, and either of these above 1 raises RooflineError:
+      * executed.frac = PMC VALU lane-instructions per nonce (this code
+        object's summary) x this run's kernel rate / peak;
+      * work_bound.frac = the per-nonce loop VALU of the variants this
+        workload runs (tools/variant_report.py: the loop alone, a floor on
+        what a nonce executes) x this run's kernel rate / peak."""
+    for path, d in (("roofline.executed", roof.get("executed")), ("roofline.work_bound", roof.get("work_bound"))):
+        v = d.get("frac") if isinstance(d, dict) else None
         if isinstance(v, (int, float)) and v > 1.0:
-            roof["stale_profile"] = {k: roof.pop(k), "source": roof.get("rocprof_source"),
-                                     "note": "the committed rocprofv3 average is shorter than this config's "
-                                             "work allows: the profile is stale (older build or plan)"}
-    stack = [("roofline", roof)]
-    while stack:
-        path, d = stack.pop()
-        for k, v in d.items():
-            if isinstance(v, dict):
-                if k != "stale_profile":
-                    stack.append((f"{path}.{k}", v))
-            elif (k == "frac" or k.startswith("frac_")) and isinstance(v, (int, float)) and v > 1.0:
-                raise RooflineError(f"{path}.{k} = {v:.4f} > 1 on a 1-block config")
+            raise RooflineError(f"{path}.frac = {v:.4f} > 1: the kernel rate exceeds what its own instruction "
+                                f"count allows at the {VALU_PEAK_OPS / 1e12:.2f} T peak")
 
 
-def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof=(None, None), single_gpu=True):
+def clock_from_stamps(before, after, wall_hz):
+    """Average shader clock of each XCC between two clock-probe stamps
+    (tools/clock_probe.hip): the s_memtime midpoint delta over the
+    s_memrealtime delta x the wall-counter rate.  before / after: one
+    (memtime, memrealtime, memtime, xcc) per workgroup; the first workgroup
+    seen on each XCC is its sample.  None when no XCC pairs up."""
+    def first(stamps):
+        out = {}
+        for t0, r, t1, x in stamps:
+            out.setdefault(int(x), ((t0 + t1) / 2.0, r))
+        return out
+
+    b, a = first(before), first(after)
+    per, span = {}, []
+    for x in sorted(set(a) & set(b)):
+        dt, dr = a[x][0] - b[x][0], a[x][1] - b[x][1]
+        if dt > 0 and dr > 0:
+            per[x] = dt * wall_hz / dr / 1e9
+            span.append(dr / wall_hz)
+    if not per:
+        return None
+    v = list(per.values())
+    return {"mean_GHz": sum(v) / len(v), "min_GHz": min(v), "max_GHz": max(v),
+            "per_xcc_GHz": {str(k): per[k] for k in per}, "interval_s": max(span)}
+
+
+CLOCK_PROBE_LIB = os.path.join(ROOT, "tools", "libp1clock.so")
+
+
+class ClockProbe:
+    """Shader-clock stamps of every XCD of the given devices
+    (tools/libp1clock.so, tools/clock_probe.hip), taken just outside the
+    timed steps on a stream of its own: the timed kernels are untouched.
+    Measurement only: without the library the line reports no clock and
+    says why."""
+    NBLOCKS = 64  # workgroups per stamp: 8 per XCD under round-robin dispatch
+
+    def __init__(self, devices, path=CLOCK_PROBE_LIB):
+        import ctypes
+
+        self.devices, self.lib, self.error = list(devices), None, None
+        if not os.path.exists(path):
+            self.error = f"{os.path.relpath(path, ROOT)} not built"
+            return
+        lib = ctypes.CDLL(path)
+        lib.p1clk_stamp.restype = ctypes.c_int
+        lib.p1clk_stamp.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong)]
+        lib.p1clk_wall_rate_khz.restype = ctypes.c_int
+        lib.p1clk_wall_rate_khz.argtypes = [ctypes.c_int]
+        self.lib = lib
+
+    def stamp(self):
+        """{device: [(memtime, memrealtime, memtime, xcc)] per workgroup} or None"""
+        import ctypes
+
+        if self.lib is None:
+            return None
+        out = {}
+        for d in self.devices:
+            buf = (ctypes.c_ulonglong * (4 * self.NBLOCKS))()
+            rc = self.lib.p1clk_stamp(d, self.NBLOCKS, buf)
+            if rc != 0:
+                self.error = f"p1clk_stamp(device {d}) returned hipError {rc}"
+                return None
+            out[d] = [tuple(buf[4 * i:4 * i + 4]) for i in range(self.NBLOCKS)]
+        return out
+
+    def clock(self, before, after):
+        """The `clock` record of the interval between two stamps."""
+        if before is None or after is None:
+            return {"effective_clock_GHz": None, "error": self.error or "no stamps"}
+        devs = {}
+        for d in self.devices:
+            khz = self.lib.p1clk_wall_rate_khz(d)
+            c = clock_from_stamps(before.get(d, []), after.get(d, []), khz * 1e3) if khz > 0 else None
+            devs[str(d)] = dict(c, wall_counter_kHz=khz) if c else {"error": f"no XCC pairs (wall {khz} kHz)"}
+        means = [c["mean_GHz"] for c in devs.values() if "mean_GHz" in c]
+        ghz = sum(means) / len(means) if means else None
+        rec = {"effective_clock_GHz": ghz, "devices": devs,
+               "method": "tools/clock_probe.hip stamps before and after the timed steps: delta s_memtime "
+                         "(shader cycles) / delta s_memrealtime x its rate, per XCC, mean over XCCs and devices "
+                         "(MI355X_MICROARCH.md 'DVFS give-back' item 6)"}
+        if ghz is not None and not 0.3 < ghz < 3.0:
+            rec["implausible"] = True
+        return rec
+
+
+def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof=(None, None), single_gpu=True,
+                      codeobj=None, clock=None):
     """The bench line's `roofline` block for the dominant kernel k_scan.
 
     achieved = algorithmic ops (1384 x B_tail per nonce) /
     the HIP-event duration of the launches (stats: scan_alg_ops,
     scan_kernel_ms, scan_launches, scan_nonces summed over this process's
     devices); peak = 78.64 T int32 lane-ops/s.  Beside it: frac_rocprof (the
-    same ops over the committed rocprofv3 average of this config's timed
-    launches, single GPU only), the executed-instruction fraction from the
-    PMC summary, and the loop-mix issue fraction."""
+    same ops over the rocprofv3 average of this config's timed launches,
+    single GPU only), the executed-instruction fraction from the PMC
+    summary and the loop-mix issue fraction -- each from a profile of THIS
+    code object (`codeobj`, sha256) or null with profile_stale -- and, with
+    `clock` (ClockProbe.clock), the sustained shader clock of the timed
+    steps and the fraction of the peak at that clock."""
     k_ms = stats["scan_kernel_ms"]
     k_n = stats["scan_launches"]
     achieved = stats["scan_alg_ops"] / (k_ms * 1e-3) if k_ms > 0 else 0.0
     k_rate = stats["scan_nonces"] / (k_ms * 1e-3) if k_ms > 0 else 0.0  # nonces/s per device
+    lo = cfg.get("lo", 0)
+    hi = cfg["hi"] if "hi" in cfg else job_total(cfg, 1) - 1
     roof = {
         "bound": "valu-int32",
         "achieved": achieved / 1e12,
         "peak": VALU_PEAK_OPS / 1e12,
         "unit": "TOP/s",
         "frac": achieved / VALU_PEAK_OPS,
+        "frac_kind": "algorithmic ops (SURVEY.md 8(d)) per second / peak: a speed ratio, not a utilisation -- "
+                     "hoisting lets a layout exceed 1; the work bound is `work_bound` / `executed`",
         "peak_basis": "256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md; tools/valu_peak); "
                       "supersedes SURVEY.md 8(d)'s 39.32 T",
         "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
@@ -426,7 +550,16 @@ def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof
         "launches_per_step": k_n / steps if steps else None,
         "kernel_hashes_per_s_G": k_rate / 1e9,
         "fast_nonce_share": stats["fast_nonces"] / max(1, stats["fast_nonces"] + stats["generic_nonces"]),
+        "codeobj_sha256": codeobj,
     }
+    line_clk = clock.get("effective_clock_GHz") if clock and not clock.get("implausible") else None
+    if clock is not None:
+        roof["clock"] = clock
+        roof["effective_clock_GHz"] = line_clk
+        if line_clk:
+            # the same algorithmic rate against the peak at the clock the
+            # chip actually sustained over the timed steps (DVFS)
+            roof["frac_at_sustained_clock"] = achieved / (VALU_PEAK_OPS * line_clk / 2.4)
     if pmc and pmc.get("write_bytes_per_launch_calibrated") is not None:
         # WRITE_SIZE counts k_scan's 16-B-per-workgroup partial stores 2x
         # (profiles/r04c_wcal.json): the calibrated bytes against the
@@ -435,13 +568,21 @@ def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof
         roof["alg_bytes_per_launch"] = pmc.get("partials_bytes_per_launch")
         roof["traffic_note"] = pmc.get("traffic_note")
     avg_ns, src = rocprof
-    if single_gpu and avg_ns and k_n:
-        # one launch of this config's plan; rocprofv3 --kernel-trace average
-        # of the same command's timed launches
-        roof["frac_rocprof"] = stats["scan_alg_ops"] / k_n / (avg_ns * 1e-9) / VALU_PEAK_OPS
-        roof["rocprof_avg_launch_ms"] = avg_ns / 1e6
+    stale = []
+    if single_gpu:
+        roof["frac_rocprof"] = None
         roof["rocprof_source"] = src
-    if pmc and pmc.get("valu_wave_instr_per_nonce"):
+        if avg_ns and k_n:
+            # one launch of this config's plan; rocprofv3 --kernel-trace
+            # average of the same command's timed launches, same code object
+            roof["frac_rocprof"] = stats["scan_alg_ops"] / k_n / (avg_ns * 1e-9) / VALU_PEAK_OPS
+            roof["rocprof_avg_launch_ms"] = avg_ns / 1e6
+        else:
+            stale.append("rocprof")
+    roof["executed"] = None
+    if not pmc:
+        stale.append("pmc")
+    elif pmc.get("valu_wave_instr_per_nonce"):
         # SURVEY.md 8(d) accounting rule: the executed-instruction fraction
         # SQ_INSTS_VALU x 64 / (t x peak), this run's kernel rate x the PMC
         # instructions per nonce
@@ -456,12 +597,14 @@ def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof
             "note": "frac counts executed VALU lane-instructions against the same 78.6 T peak "
                     "(SURVEY.md 8(d) accounting rule)",
         }
-        msg = cfg["msg"]
-        mix_ab = workload_mix(len(msg), 0, job_total(cfg, 1) - 1)
+        if line_clk:
+            ex["frac_at_sustained_clock"] = ex["frac"] * 2.4 / line_clk
+        mix_ab = workload_mix(len(cfg["msg"]), lo, hi)
         if mix_ab and k_rate > 0:
             # the executed loop mix at its ideal issue rate vs the SIMD
-            # cycles this run spent per wave-iteration (64 nonces)
-            clk = (pmc.get("effective_clock_GHz") or 2.4) * 1e9
+            # cycles this run spent per wave-iteration (64 nonces), at this
+            # run's own clock when the probe measured it
+            clk = (line_clk or pmc.get("effective_clock_GHz") or 2.4) * 1e9
             spent = 1024 * clk * 64 / k_rate
             # DESIGN.md 4 "Dual issue": one VALU issue slot per SIMD per
             # SLOT_CYCLES; a half-rate op issues only as the first op of a
@@ -470,6 +613,7 @@ def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof
             # max(A, (A + B) / 2) slots
             ideal = SLOT_CYCLES * max(mix_ab[0], (mix_ab[0] + mix_ab[1]) / 2.0)
             ex["mix_issue_frac"] = ideal / spent
+            ex["mix_issue_clock"] = "this run (clock probe)" if line_clk else "PMC session"
             ex["loop_mix_per_nonce"] = {"half_rate_A": mix_ab[0], "full_rate_B": mix_ab[1],
                                         "source": VARIANT_PROFILE}
             ex["mix_issue_note"] = ("fewest SIMD cycles the loop mix can issue in (4 x max(A, (A + B) / 2): "
@@ -485,22 +629,38 @@ def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof
                 ex["dual_issue"] = {"valu2_per_valu": v2, "valu_ops_in_shared_slots": 2.0 * v2,
                                     "shared_slot_bound": 2.0 * min(mix_ab[1], n_ab / 2.0) / n_ab,
                                     "slot_model_simd_cycles_per_valu": 4.0 * (1.0 - v2),
+                                    "source": pmc_src,
                                     "note": "SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU from the PMC summary; a slot holds "
                                             "one op of any class first and a full-rate op of another wave second, "
                                             "so at most 2 x min(B, (A+B)/2) / (A+B) of the ops can share a slot"}
         roof["executed"] = ex
+    if stale:
+        # no profile of THIS code object: its fields stay null rather than
+        # borrowing another build's numbers
+        roof["profile_stale"] = True
+        roof["profile_missing"] = stale
+    mix_w = workload_mix(len(cfg["msg"]), lo, hi)
+    if mix_w and k_rate > 0:
+        ipn_loop = mix_w[0] + mix_w[1]
+        roof["work_bound"] = {"loop_valu_per_nonce": ipn_loop, "frac": ipn_loop * k_rate / VALU_PEAK_OPS,
+                              "source": VARIANT_PROFILE,
+                              "note": "per-nonce loop VALU of the variants this workload runs x this run's kernel "
+                                      "rate / peak: a floor on the executed fraction; above 1 the line is refused"}
     if cfg["b_tail"] != 1:
         # the algorithmic count charges both tail blocks per nonce; the kernel
         # compresses the hi-digit block once per 10^k nonces and reads the
         # lo-only block's schedule from a table (MODE 5): the algorithmic
         # rate is not a utilisation, so it is not called a fraction here
         roof["alg_ops_over_peak"] = roof.pop("frac")
-        roof["frac"] = roof.get("executed", {}).get("frac")
+        roof.pop("frac_kind")
+        roof["frac"] = (roof.get("executed") or {}).get("frac")
         roof["frac_basis"] = ("executed VALU lane-instructions (PMC) / peak: for this 2-block config the "
                               "algorithmic count overstates the work (block 0 once per 10^k nonces, block 1's "
                               "schedule tabulated), see alg_ops_over_peak")
         if "frac_rocprof" in roof:
             roof["alg_ops_over_peak_rocprof"] = roof.pop("frac_rocprof")
+        if "frac_at_sustained_clock" in roof:
+            roof["alg_ops_over_peak_at_sustained_clock"] = roof.pop("frac_at_sustained_clock")
     mix = mix_roofline()
     if mix and k_ms > 0:
         mix["peak_GH_s"] = mix["peak_GH_s_per_block"] / cfg["b_tail"]
@@ -509,32 +669,46 @@ def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof
                        "instruction at its own measured peak: a speed ratio, not a utilisation (the kernel "
                        "hoists per-thread rounds and schedule words, so it can exceed 1)")
         roof["unhoisted_mix"] = mix
-    check_fracs(roof, cfg["b_tail"])
+    check_work_bound(roof)
     return roof
 
 
-SHARD_BALANCE_PROFILE = "profiles/r03h_shard_balance.jsonl"
-
-
-def scaling_expectation(config, n):
-    """What an N-GPU c4 run should reach if every GPU runs like the one the
-    shards were measured on: 2^38 / the slowest plan_shards shard, each shard
-    timed alone on one GPU (tools/shard_balance.py).  None for other configs
-    or N without a measurement."""
+def scaling_expectation(config, n, codeobj=None):
+    """What an N-GPU c4 run should reach if every GPU runs like the one this
+    code object was profiled on: N x the one-GPU rate of the committed
+    rocprofv3 c4 trace of THIS code object (2^38 / its average timed
+    launch), divided by the slowest-over-mean shard time of N plan_shards
+    shards, each timed alone on one GPU (tools/shard_balance.py, the newest
+    profiles/*_shard_balance.jsonl).  Falls back to that file's own
+    implied rate (its build's) when this code object has no c4 trace.  None
+    for other configs or N without a balance measurement."""
     if config != "c4" or n < 2:
         return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_shard_balance.jsonl")), key=profile_tag_key)
+    if not files:
+        return None
     try:
-        with open(os.path.join(ROOT, SHARD_BALANCE_PROFILE)) as f:
-            for line in f:
-                d = json.loads(line)
-                if d.get("n") == n and d.get("split") == "plan_shards":
-                    return {"implied_GH_s": d["implied_GH_s"], "slowest_shard_over_mean": d["max_over_mean"],
-                            "shard_kernel_ms": d["kernel_ms"], "source": SHARD_BALANCE_PROFILE,
-                            "note": "2^38 / the slowest of this N's plan_shards shards, each timed alone on "
-                                    "one GPU; a shortfall against it is cross-GPU (see per_gpu)"}
-    except (OSError, ValueError, KeyError):
-        pass
-    return None
+        with open(files[-1]) as f:
+            rows = [json.loads(ln) for ln in f if ln.startswith("{")]
+    except (OSError, ValueError):
+        return None
+    row = next((d for d in rows if d.get("n") == n and d.get("split") == "plan_shards"), None)
+    if row is None:
+        return None
+    m = row["max_over_mean"]
+    out = {"slowest_shard_over_mean": m, "shard_kernel_ms": row.get("kernel_ms"),
+           "balance_source": os.path.relpath(files[-1], ROOT)}
+    avg_ns, src = rocprof_row("c4", codeobj)
+    if avg_ns:
+        one = CONFIGS["c4"]["total"] / (avg_ns * 1e-9) / 1e9
+        out.update(implied_GH_s=n * one / m, one_gpu_GH_s=one, one_gpu_source=src,
+                   note="N x this code object's one-GPU c4 kernel rate (rocprofv3 trace) / the slowest "
+                        "plan_shards shard over the mean; a shortfall against it is cross-GPU (see per_gpu)")
+    else:
+        out.update(implied_GH_s=row["implied_GH_s"], one_gpu_source=None,
+                   note="2^38 / the slowest plan_shards shard timed alone on one GPU, on the build of "
+                        "balance_source (no c4 trace of this code object is committed)")
+    return out
 
 
 def device_identity(index):
@@ -593,10 +767,14 @@ class Progress:
             self.last = now
 
 
-def timed_steps(step, steps, warmup, barrier, progress=None):
+def timed_steps(step, steps, warmup, barrier, progress=None, probe=None):
     """W untimed steps, then K timed ones bracketed by barrier() (a
     torch.distributed barrier + device synchronise); library stats reset and
-    HIP-event profiling on over exactly the timed steps."""
+    HIP-event profiling on over exactly the timed steps.  With a ClockProbe,
+    one clock stamp just before the opening barrier and one just after the
+    closing one: the sustained shader clock of the timed steps (the stamps
+    themselves are outside the timed region).  Returns (elapsed, step_ms,
+    results, stats, clock)."""
     import p1_amd
 
     progress = progress or (lambda *a: None)
@@ -605,6 +783,7 @@ def timed_steps(step, steps, warmup, barrier, progress=None):
         progress("warm-up step", i + 1, warmup)
     p1_amd.reset_stats()
     p1_amd.set_profiling(True)
+    before = probe.stamp() if probe else None
     barrier()
     t0 = time.perf_counter()
     results, marks = [], [t0]
@@ -614,16 +793,20 @@ def timed_steps(step, steps, warmup, barrier, progress=None):
         progress("timed step", i + 1, steps)  # a few µs between steps, after the mark
     barrier()
     elapsed = time.perf_counter() - t0
+    after = probe.stamp() if probe else None
     p1_amd.set_profiling(False)
     step_ms = sorted((b - a) * 1e3 for a, b in zip(marks, marks[1:]))
-    return elapsed, step_ms, results, p1_amd.get_stats()
+    clock = probe.clock(before, after) if probe else None
+    if clock is not None:
+        clock["timed_region_s"] = elapsed
+    return elapsed, step_ms, results, p1_amd.get_stats(), clock
 
 
 # by_config sub-results of the N = 1 line: (config, warmup, steps)
 SUB_CONFIGS = [("c2", 2, 5), ("c3", 1, 3)]
 
 
-def sub_result(name, warmup, steps, sync):
+def sub_result(name, warmup, steps, sync, codeobj=None, probe=None):
     """One other BASELINE config timed on the same device after the headline
     run: value, ms_per_step, the roofline fraction and the check against its
     independently pinned answer."""
@@ -631,10 +814,11 @@ def sub_result(name, warmup, steps, sync):
 
     cfg = CONFIGS[name]
     total = job_total(cfg, 1)
-    elapsed, step_ms, results, stats = timed_steps(lambda: p1_amd.scan(cfg["msg"], 0, total - 1), steps, warmup,
-                                                   sync, Progress(name))
-    pmc, pmc_src = pmc_summary(name)
-    roof = assemble_roofline(name, cfg, stats, steps, pmc, pmc_src, rocprof_row(name))
+    elapsed, step_ms, results, stats, clock = timed_steps(lambda: p1_amd.scan(cfg["msg"], 0, total - 1), steps,
+                                                          warmup, sync, Progress(name), probe)
+    pmc, pmc_src = pmc_summary(name, codeobj)
+    roof = assemble_roofline(name, cfg, stats, steps, pmc, pmc_src, rocprof_row(name, codeobj), codeobj=codeobj,
+                             clock=clock)
     known, src = known_answer(cfg, 1)
     res = results[-1]
     out = {"workload": cfg["desc"], "value": total * steps / elapsed / 1e9, "unit": "GH/s",
@@ -642,9 +826,13 @@ def sub_result(name, warmup, steps, sync):
            "kernel_hashes_per_s_G": roof["kernel_hashes_per_s_G"], "avg_launch_ms": roof["avg_launch_ms"],
            "frac": roof["frac"], "result": list(res), "consistent": all(r == res for r in results),
            "matches_known": (tuple(res) == tuple(known)) if known else None, "known_source": src}
-    for k in ("frac_rocprof", "alg_ops_over_peak", "frac_basis"):
+    for k in ("frac_rocprof", "alg_ops_over_peak", "alg_ops_over_peak_rocprof", "frac_basis", "rocprof_source",
+              "effective_clock_GHz", "frac_at_sustained_clock", "profile_stale"):
         if k in roof:
             out[k] = roof[k]
+    ex = roof.get("executed") or {}
+    out["executed_frac"] = ex.get("frac")
+    out["pmc_source"] = ex.get("source")
     return out
 
 
@@ -655,6 +843,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
                     help="default: c4 (configs[3], the fixed [0,2^38) job) at every N")
+    ap.add_argument("--layout", default=None, metavar="L,START[,N]",
+                    help="profile one tail layout instead of a BASELINE config (tools/sweep.py message of L bytes, "
+                         "nonces [START, START+N), N default 2^32)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-small-request", action="store_true",
@@ -694,7 +885,15 @@ def main():
     except UsageError as e:
         print(str(e), file=sys.stderr)
         sys.exit(2)
-    cfg = CONFIGS[run["config"]]
+    if args.layout:
+        try:
+            cfg = layout_config(args.layout)
+        except UsageError as e:
+            print(str(e), file=sys.stderr)
+            sys.exit(2)
+        run["config"] = "L%dd%d" % tuple(cfg["layout"])
+    else:
+        cfg = CONFIGS[run["config"]]
     mode, n_gpus, rank, world = run["mode"], run["n"], run["rank"], run["world"]
 
     import torch.distributed as dist
@@ -703,6 +902,7 @@ def main():
 
     msg = cfg["msg"]
     total = job_total(cfg, n_gpus)
+    base = cfg.get("lo", 0)  # first nonce of the job
     t_init = time.perf_counter()  # device init, module load, communicators: reported, not timed
     if mode == "torchrun":
         gpu = run["local_rank"] % visible if args.dist_backend == "gloo" else run["local_rank"]
@@ -729,14 +929,18 @@ def main():
             print(str(e), file=sys.stderr)
             sys.exit(5)
     init_ms = (time.perf_counter() - t_init) * 1e3
+    codeobj = p1_amd.codeobj_sha256()
+    # HIP ordinals of the devices this process scans on, for the clock probe
+    ordinals = [gpu] if mode == "torchrun" else [p1_amd.device_info(i)["ordinal"] for i in devices]
+    probe = ClockProbe(ordinals)
 
     timing = {}  # torchrun: this rank's scan / all-gather time of the timed steps
 
     def step():
         if mode == "torchrun":
-            return distributed_scan(msg, 0, total - 1, p1_amd.scan, device=coll_dev, shard_fn=p1_amd.plan_shards,
+            return distributed_scan(msg, base, base + total - 1, p1_amd.scan, device=coll_dev, shard_fn=p1_amd.plan_shards,
                                     timing=timing)
-        return p1_amd.scan(msg, 0, total - 1)  # library: shards + RCCL all-gather inside
+        return p1_amd.scan(msg, base, base + total - 1)  # library: shards + RCCL all-gather inside
 
     def barrier():
         if mode == "torchrun":
@@ -749,7 +953,7 @@ def main():
         step()
         progress("warm-up step", i + 1, args.warmup)
     timing.clear()
-    elapsed, step_ms, results, stats = timed_steps(step, args.steps, 0, barrier, progress)
+    elapsed, step_ms, results, stats, clock = timed_steps(step, args.steps, 0, barrier, progress, probe)
 
     if mode == "torchrun":
         from p1_amd.dist import gather_rank_identity, gather_rank_stats
@@ -793,10 +997,11 @@ def main():
         hashes = total * args.steps
         value = hashes / elapsed / 1e9
         ms_per_step = elapsed * 1e3 / args.steps
-        pmc, pmc_src = pmc_summary(run["config"])
+        pmc, pmc_src = pmc_summary(run["config"], codeobj)
         try:
             roofline = assemble_roofline(run["config"], cfg, stats, args.steps, pmc, pmc_src,
-                                         rocprof_row(run["config"]), single_gpu=(n_gpus == 1))
+                                         rocprof_row(run["config"], codeobj), single_gpu=(n_gpus == 1),
+                                         codeobj=codeobj, clock=clock)
         except RooflineError as e:
             # the line is still printed (minutes of timing are not thrown
             # away), the error named in it, and the exit status says so
@@ -835,32 +1040,36 @@ def main():
                 "config": run["config"],
                 "msg_len": len(msg),
                 "nonces_per_gpu": total // n_gpus,
-                "job_range": [0, total - 1],
+                "job_range": [base, base + total - 1],
                 "parallelism": parallelism,
                 "launch": mode,
                 "devices": devices if mode != "torchrun" else f"one per rank, {world} ranks",
             },
             "test_knobs": knobs,
-            "library": {"path": os.path.relpath(p1_amd.lib_path(), ROOT), "version": p1_amd.version()},
+            "library": {"path": os.path.relpath(p1_amd.lib_path(), ROOT), "version": p1_amd.version(),
+                        "codeobj_sha256": codeobj},
             "topology": topology,
-            "scaling_expectation": scaling_expectation(run["config"], n_gpus),
+            "scaling_expectation": scaling_expectation(run["config"], n_gpus, codeobj),
             "roofline": roofline,
             "per_gpu": scaling_report(units, args.steps, ms_per_step),
             "result": {"hash": result[0], "nonce": result[1], "consistent": consistent,
                        "matches_known": (tuple(result) == tuple(known)) if known else None,
                        "known": list(known) if known else None, "known_source": known_src},
         }
-        if n_gpus == 1 and mode != "torchrun" and not args.no_by_config:
+        if "layout" in cfg:
+            line["config"].update(layout=cfg["layout"], variant=cfg["variant"], b_tail=cfg["b_tail"])
+        if n_gpus == 1 and mode != "torchrun" and not args.no_by_config and "layout" not in cfg:
             # the other BASELINE configs on the same GPU, after the timed
             # headline run (never inside it)
             line["by_config"] = {run["config"]: {"value": value, "ms_per_step": ms_per_step,
                                                  "frac": roofline.get("frac"),
+                                                 "effective_clock_GHz": roofline.get("effective_clock_GHz"),
                                                  "matches_known": line["result"]["matches_known"],
                                                  "headline": True}}
             for name, w, k in SUB_CONFIGS:
                 if name != run["config"]:
                     try:
-                        line["by_config"][name] = sub_result(name, w, k, barrier)
+                        line["by_config"][name] = sub_result(name, w, k, barrier, codeobj, probe)
                     except RooflineError as e:
                         line["by_config"][name] = {"error": str(e)}
                         roof_failed.append(f"{name}: {e}")

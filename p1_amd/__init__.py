@@ -29,5 +29,7 @@ from ._lib import (  # noqa: F401
     test_knobs,
     shutdown,
     version,
+    codeobj_bytes,
+    codeobj_sha256,
 )
 from .sharding import shard_range, combine_keys  # noqa: F401

@@ -254,3 +254,24 @@ def shutdown():
 
 def version():
     return load().p1hip_version().decode()
+
+
+def codeobj_bytes(lib=None):
+    """The gfx950 code object embedded in the library (the bytes between the
+    p1hip_kernels_co / p1hip_kernels_co_end symbols of
+    csrc/p1hip_kernels_blob.S, i.e. build/p1hip_kernels.hsaco as linked):
+    the exact kernels every scan through this library runs."""
+    lib = lib or load()
+    start = ctypes.addressof(ctypes.c_char.in_dll(lib, "p1hip_kernels_co"))
+    end = ctypes.addressof(ctypes.c_char.in_dll(lib, "p1hip_kernels_co_end"))
+    if end <= start:
+        raise P1HipError(-100, "embedded code object is empty")
+    return ctypes.string_at(start, end - start)
+
+
+def codeobj_sha256(lib=None):
+    """sha256 (hex) of the embedded code object: the key that ties a rocprof
+    or PMC summary under profiles/ to the kernels it measured."""
+    import hashlib
+
+    return hashlib.sha256(codeobj_bytes(lib)).hexdigest()

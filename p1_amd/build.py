@@ -9,7 +9,7 @@ import subprocess
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARTEFACTS = ["p1_amd/libp1hip.so", "oracle/libp1oracle.so", "p1_amd/p1miner", "p1_amd/p1server", "p1_amd/p1client",
-             "tools/p1emu", "tools/lsp_scenarios", "tools/lsp_fake_miner"]
+             "tools/p1emu", "tools/lsp_scenarios", "tools/lsp_fake_miner", "tools/libp1clock.so"]
 
 
 def missing():

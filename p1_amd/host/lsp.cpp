@@ -117,15 +117,22 @@ void on_ack(Peer& p, int64_t seq, int window, const SendFn& send) {
 // A server also caps the early bytes of ALL its connections together
 // (kMaxEarlyBytesAll, `pool`): a connection costs one unauthenticated Connect,
 // so a per-connection cap alone would let many of them hold 64 MB each.
+// And per source host (kMaxEarlyBytesHost, `host_pool`): without it one
+// peer opening 4 connections from 4 ports fills the whole pool, and every
+// other connection's out-of-order Data is then dropped until those time out
+// (ADVICE r05).  A host's connections together hold what one may.
 constexpr int64_t kMaxEarly = 1 << 16;
 constexpr size_t kMaxEarlyBytes = 64u << 20;
 constexpr size_t kMaxEarlyBytesAll = 256u << 20;
-void on_data(Peer& p, Message& m, int window, const SendFn& send, const DeliverFn& deliver, size_t* pool = nullptr) {
+constexpr size_t kMaxEarlyBytesHost = kMaxEarlyBytes;
+void on_data(Peer& p, Message& m, int window, const SendFn& send, const DeliverFn& deliver, size_t* pool = nullptr,
+             size_t* host_pool = nullptr) {
   (void)window;
   if (m.SeqNum >= p.expect + kMaxEarly) return;
   if (m.SeqNum > p.expect && !p.early.count(m.SeqNum) &&
       (p.early_bytes + m.Payload.size() > kMaxEarlyBytes ||
-       (pool && *pool + m.Payload.size() > kMaxEarlyBytesAll)))
+       (pool && *pool + m.Payload.size() > kMaxEarlyBytesAll) ||
+       (host_pool && *host_pool + m.Payload.size() > kMaxEarlyBytesHost)))
     return;
   send(NewAck(p.conn_id, m.SeqNum));
   p.got_data = true;
@@ -136,6 +143,7 @@ void on_data(Peer& p, Message& m, int window, const SendFn& send, const DeliverF
     if (p.early.emplace(m.SeqNum, std::move(payload)).second) {
       p.early_bytes += n;
       if (pool) *pool += n;
+      if (host_pool) *host_pool += n;
     }
     return;
   }
@@ -144,6 +152,7 @@ void on_data(Peer& p, Message& m, int window, const SendFn& send, const DeliverF
   for (auto it = p.early.find(p.expect); it != p.early.end(); it = p.early.find(p.expect)) {
     p.early_bytes -= it->second.size();
     if (pool) *pool -= it->second.size();
+    if (host_pool) *host_pool -= it->second.size();
     deliver(std::move(it->second));
     p.early.erase(it);
     p.expect++;
@@ -450,8 +459,15 @@ class ServerImpl : public Server {
  private:
   struct Conn {
     Peer p;
+    std::string host;      // source address without the port (kMaxEarlyBytesHost)
     bool closing = false;  // CloseConn / Close: drain pending, deliver nothing
   };
+
+  static std::string host_of(const lspnet::UDPAddr& a) {
+    std::string s = a.String();
+    const size_t colon = s.rfind(':');
+    return colon == std::string::npos ? s : s.substr(0, colon);
+  }
   struct Event {
     int64_t conn;
     std::string payload;
@@ -479,6 +495,7 @@ class ServerImpl : public Server {
         Conn c;
         c.p.conn_id = id;
         c.p.addr = from;
+        c.host = host_of(from);
         c.p.copies = prm_.Copies > 1 ? prm_.Copies : 1;
         conns_.emplace(id, std::move(c));
         by_addr_[from] = id;
@@ -511,7 +528,7 @@ class ServerImpl : public Server {
           [this, hide, id](std::string&& s) {
             if (!hide) inbox_.push_back({id, std::move(s), false});
           },
-          &early_all_);
+          &early_all_, &early_by_host_[c.host]);
       cv_.notify_all();
     }
   }
@@ -537,6 +554,8 @@ class ServerImpl : public Server {
       auto a = by_addr_.find(c.p.addr);
       if (a != by_addr_.end() && a->second == c.p.conn_id) by_addr_.erase(a);
       early_all_ -= c.p.early_bytes;  // its held-back data leaves with it
+      auto h = early_by_host_.find(c.host);
+      if (h != early_by_host_.end() && (h->second -= c.p.early_bytes) == 0) early_by_host_.erase(h);
       it = conns_.erase(it);
       changed = true;
     }
@@ -559,6 +578,7 @@ class ServerImpl : public Server {
   std::deque<Event> inbox_;
   int64_t next_id_ = 1;
   size_t early_all_ = 0;  // early bytes held by all connections (kMaxEarlyBytesAll)
+  std::map<std::string, size_t> early_by_host_;  // early bytes per source host (kMaxEarlyBytesHost)
   bool closing_all_ = false, lost_while_closing_ = false, closed_ = false;
   std::unique_ptr<Loop> loop_;  // last: stopped first
 };

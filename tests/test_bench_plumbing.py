@@ -153,19 +153,119 @@ def test_roofline_assembly_round5_c4_dual_issue_fields():
         assert abs(d["slot_model_simd_cycles_per_valu"] - 4 * (1 - 0.385)) < 1e-9
 
 
-def test_roofline_assembly_rejects_frac_above_one():
-    # the same 2^38 nonces "in" 2 s would be 1.9x the peak: refused, not printed
+def test_roofline_assembly_rejects_work_above_peak():
+    """the refusal is on instructions the kernel must
+    execute, not on the algorithmic ratio.  The same 2^38 nonces "in" 2 s
+    would need the c4 loops' own VALU count at 2x the peak: refused."""
     cfg = bench.CONFIGS["c4"]
-    with pytest.raises(bench.RooflineError):
+    if bench.workload_mix(len(cfg["msg"]), 0, (1 << 38) - 1) is None:
+        pytest.skip("variant reports not committed")
+    with pytest.raises(bench.RooflineError, match="work_bound"):
         bench.assemble_roofline("c4", cfg, _stats(1 << 38, 2000.0), 1)
-    # a committed rocprof average too short for the work (a stale profile) is
-    # flagged beside the line, not a refusal of this run's own numbers
-    roof = bench.assemble_roofline("c2", bench.CONFIGS["c2"], _stats(1 << 32, 117.0), 1, rocprof=(30e6, "z"))
-    assert "frac_rocprof" not in roof and roof["stale_profile"]["frac_rocprof"] > 1.0
-    assert 0.6 < roof["frac"] < 0.7
+
+
+def test_sweep_layout_above_one_algorithmically_passes():
+    """The r05af sweep's fastest one-block layout (L = 38, d = 16, variant
+    [13,6]: 59.79 GH/s, algorithmic frac 1.052; profiles/r05af_layout_sweep.jsonl)
+    is a correct run: rounds 0..12 are hoisted, so its loop executes 1035
+    VALU per nonce, 0.79 of the peak at that rate.  The line passes with the
+    algorithmic ratio above 1 named as a speed ratio."""
+    lo = 10 ** 15
+    cfg = {"msg": b"m" * 38, "b_tail": 1, "lo": lo, "hi": lo + (1 << 32) - 1}
+    assert bench.fast_variant(38, 16) == (13, 6, False)
+    ms = (1 << 32) / 59.79169752156909e9 * 1e3
+    roof = bench.assemble_roofline("sweep", cfg, _stats(1 << 32, ms), 1)
+    assert abs(roof["frac"] - 1.0522) < 1e-3 and "speed ratio" in roof["frac_kind"]
+    wb = roof.get("work_bound")
+    if wb is not None:  # needs the committed variant reports
+        assert wb["loop_valu_per_nonce"] < 1100 and 0.7 < wb["frac"] < 0.9
+
+
+def test_executed_fraction_above_one_is_refused():
+    """A PMC instruction count that this run's rate would execute above the
+    peak (executed frac 1.1) means the kernel did not do the work: refused."""
+    cfg = bench.CONFIGS["c4"]
+    ms = 5188.0
+    rate = (1 << 38) / (ms * 1e-3)
+    pmc = {"valu_wave_instr_per_nonce": 1.1 * bench.VALU_PEAK_OPS / rate, "effective_clock_GHz": 2.35}
+    with pytest.raises(bench.RooflineError, match="executed"):
+        bench.assemble_roofline("c4", cfg, _stats(1 << 38, ms), 1, pmc, "x", (5.19e9, "y"), codeobj="h")
+    bench.check_work_bound({"frac": 1.3, "frac_rocprof": 1.2, "executed": {"frac": 0.99}})  # algorithmic: allowed
     with pytest.raises(bench.RooflineError):
-        bench.check_fracs({"a": {"frac_x": 1.01}}, 1)
-    bench.check_fracs({"a": {"frac_x": 1.01}}, 2)  # 2-block: the algorithmic count is not a utilisation
+        bench.check_work_bound({"work_bound": {"frac": 1.01}})
+
+
+def _decoys(tmp_path, specs):
+    """profiles/ with PMC summaries and kernel-trace rows named like real
+    sessions: specs = [(tag, config, sha, avg_ns)]"""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    for tag, config, sha, avg in specs:
+        (prof / f"{tag}_{config}_pmc_summary.json").write_text(
+            '{"config": "%s", "codeobj_sha256": "%s", "tag": "%s"}' % (config, sha, tag))
+        (prof / f"{tag}_{config}_kernel_stats_workload.csv").write_text(
+            '"Name","Calls","AverageNs","Codeobj_SHA256"\n'
+            '"k_scan",5,%d,"%s"\n"k_scan (launches after the first 2: timed steps)",3,%d,"%s"\n'
+            % (avg + 1, sha, avg, sha))
+    return str(tmp_path)
+
+
+def test_profiles_are_selected_by_code_object_not_name(tmp_path, monkeypatch):
+    """r05v sorts after r05ae lexically; the summary of
+    the code object the line runs is chosen, the newest session among
+    several of it, and a build with no profile gets none."""
+    root = _decoys(tmp_path, [("r05v", "c4", "old", 5213000000), ("r05ae", "c4", "new", 5247000000),
+                              ("r05z", "c4", "new", 5330000000), ("r05y", "c2", "old", 83760000)])
+    monkeypatch.setattr(bench, "ROOT", root)
+    assert bench.profile_tag_key("profiles/r05ae_c4_x") > bench.profile_tag_key("profiles/r05z_c4_x") \
+        > bench.profile_tag_key("profiles/r05v_c4_x")
+    d, src = bench.pmc_summary("c4", "new")
+    assert d["tag"] == "r05ae" and src == "profiles/r05ae_c4_pmc_summary.json"
+    assert bench.pmc_summary("c4", "old")[0]["tag"] == "r05v"
+    assert bench.rocprof_row("c4", "new") == (5247000000.0, "profiles/r05ae_c4_kernel_stats_workload.csv")
+    assert bench.pmc_summary("c4", "other") == (None, None) and bench.rocprof_row("c4", "other") == (None, None)
+    assert bench.pmc_summary("c2", "new") == (None, None)
+    assert bench.pmc_summary("c4", None) == (None, None)
+
+
+def test_no_profile_of_this_build_leaves_profile_fields_null():
+    cfg = bench.CONFIGS["c4"]
+    roof = bench.assemble_roofline("c4", cfg, _stats(1 << 38, 5188.0), 1, None, None, (None, None),
+                                   codeobj="abc")
+    assert roof["profile_stale"] is True and set(roof["profile_missing"]) == {"rocprof", "pmc"}
+    assert roof["frac_rocprof"] is None and roof["executed"] is None and roof["traffic"] is None
+    assert roof["codeobj_sha256"] == "abc" and 0.9 < roof["frac"] < 0.95
+
+
+def test_clock_from_stamps_per_xcc():
+    """Two probe stamps 100 s apart on a 100 MHz wall counter, XCC x's
+    shader counter running at 2.30 + 0.01 x GHz: each XCC's clock, the mean,
+    and the XCC's first workgroup as its sample."""
+    wall = 100e6
+    before, after = [], []
+    for b in range(64):
+        x = b % 8
+        ghz = 2.30 + 0.01 * x
+        t, r = 10 ** 9 * (x + 1) + b, 5 * 10 ** 9 + b
+        before.append((t, r, t + 40, x))
+        r2 = r + int(100 * wall)
+        t2 = t + int(100 * ghz * 1e9)
+        after.append((t2, r2, t2 + 40, x))
+    c = bench.clock_from_stamps(before, after, wall)
+    assert abs(c["per_xcc_GHz"]["3"] - 2.33) < 1e-6 and abs(c["mean_GHz"] - 2.335) < 1e-6
+    assert abs(c["interval_s"] - 100.0) < 1e-6
+    assert bench.clock_from_stamps(before, [], wall) is None
+
+
+def test_sustained_clock_fraction_in_the_line():
+    cfg = bench.CONFIGS["c4"]
+    clock = {"effective_clock_GHz": 2.35, "devices": {}}
+    roof = bench.assemble_roofline("c4", cfg, _stats(1 << 38, 5188.0), 1, codeobj="h", clock=clock)
+    assert roof["effective_clock_GHz"] == 2.35
+    assert abs(roof["frac_at_sustained_clock"] - roof["frac"] * 2.4 / 2.35) < 1e-12
+    bad = bench.assemble_roofline("c4", cfg, _stats(1 << 38, 5188.0), 1, clock={"effective_clock_GHz": 9.0,
+                                                                                "implausible": True})
+    assert bad["effective_clock_GHz"] is None and "frac_at_sustained_clock" not in bad
 
 
 def test_roofline_two_block_config_names_the_algorithmic_ratio():
@@ -177,10 +277,13 @@ def test_roofline_two_block_config_names_the_algorithmic_ratio():
 
 
 def test_rocprof_row_reads_committed_summary():
-    avg, src = bench.rocprof_row("c2")
-    # one c2 launch (2^32 nonces): no faster than the 78.6 T peak allows
-    # (75.6 ms), no slower than the round-1 kernel (~120 ms)
-    floor = (1 << 32) * 1384 / bench.VALU_PEAK_OPS * 1e9
+    """The committed c2 trace of the shipped code object (r05ag, retagged
+    with its hash) is found by that hash."""
+    sha = "ec224f858b5ed8bcd162b07001b8e08ec046635ec5397eaad68df5c39428a78a"
+    avg, src = bench.rocprof_row("c2", sha)
+    # one c2 launch (2^32 nonces): no faster than the loop's own VALU count
+    # allows at the 78.6 T peak, no slower than the round-1 kernel (~120 ms)
+    floor = (1 << 32) * 1000 / bench.VALU_PEAK_OPS * 1e9
     assert avg and floor < avg < 130e6 and src.startswith("profiles/"), (avg, src)
 
 
@@ -218,11 +321,20 @@ def test_bench_imports_torch_before_the_library():
     assert src.index("import torch\n") < src.index("import p1_amd\n")
 
 
+SHIPPED_R05 = "ec224f858b5ed8bcd162b07001b8e08ec046635ec5397eaad68df5c39428a78a"
+
+
 def test_scaling_expectation_for_the_driver_shapes():
+    """the N-GPU expectation is this code object's own
+    one-GPU c4 rate (its committed trace) x N / the plan_shards balance."""
     for n in (2, 4, 8):
-        e = bench.scaling_expectation("c4", n)
+        e = bench.scaling_expectation("c4", n, SHIPPED_R05)
         assert e and e["slowest_shard_over_mean"] < 1.01 and len(e["shard_kernel_ms"]) == n
-    assert 290 < bench.scaling_expectation("c4", 8)["implied_GH_s"] < 300
+        assert e["one_gpu_source"].endswith("_c4_kernel_stats_workload.csv") and 51 < e["one_gpu_GH_s"] < 54
+        assert abs(e["implied_GH_s"] - n * e["one_gpu_GH_s"] / e["slowest_shard_over_mean"]) < 1e-9
+    assert 405 < bench.scaling_expectation("c4", 8, SHIPPED_R05)["implied_GH_s"] < 430
+    other = bench.scaling_expectation("c4", 8, "not-profiled")
+    assert other["one_gpu_source"] is None and other["implied_GH_s"] > 0
     assert bench.scaling_expectation("c4", 1) is None and bench.scaling_expectation("c2", 8) is None
 
 

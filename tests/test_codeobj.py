@@ -285,3 +285,48 @@ def test_k_scan_registers_keep_four_waves(codeobj):
     blk = notes[notes.index(".name:           k_scan\n"):]
     get = lambda k: int(re.search(rf"\.{k}:\s+(\d+)", blk).group(1))  # noqa: E731
     assert get("vgpr_count") <= 128 and get("sgpr_count") <= 106, (get("vgpr_count"), get("sgpr_count"))
+
+
+def test_branches_fit_after_the_post_pass_growth(codeobj):
+    """Makefile -amdgpu-s-branch-bits=15: the post-pass inserts its
+    s_setprio and loop padding after LLVM relaxed the branches, so LLVM is
+    told branches reach +-2^14 dwords of the real +-2^15.  The shipped
+    object's largest displacement stays inside the real range with room to
+    spare; the per-nonce loops contain no long (s_setpc) branch."""
+    dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", codeobj], capture_output=True, text=True,
+                         check=True).stdout
+    offs = []
+    for m in re.finditer(r"\bs_(?:c)?branch\w*\s+(\d+)\s+//", dis):
+        v = int(m.group(1))
+        offs.append(v - 65536 if v >= 32768 else v)
+    assert len(offs) > 500
+    assert max(abs(v) for v in offs) < 1 << 15
+    assert dis.count("s_setprio") > 20000
+
+
+def test_assembler_rejects_a_branch_out_of_range(tmp_path):
+    """Why the branch margin is safe by construction: a short branch the
+    growth pushed out of range fails the build's assembly step (the
+    Makefile's clang -cc1as) instead of producing a wrong target."""
+    src = tmp_path / "far.s"
+    src.write_text(".text\nf:\n s_branch .Lend\n" + " s_nop 0\n" * 33000 + ".Lend:\n s_endpgm\n")
+    r = subprocess.run([f"{LLVM}/clang", "-cc1as", "-triple", "amdgcn-amd-amdhsa", "-filetype", "obj", "-target-cpu",
+                        "gfx950", "-o", str(tmp_path / "far.o"), str(src)], capture_output=True, text=True)
+    assert r.returncode != 0 and "branch size exceeds simm16" in r.stderr, r.stderr[-500:]
+
+
+def test_codeobj_sha256_is_the_embedded_object():
+    """p1_amd.codeobj_sha256 (what bench.py reports and matches profiles
+    by) hashes exactly the code object embedded in the library, which is
+    build/p1hip_kernels.hsaco when the build tree is present."""
+    import hashlib
+
+    sys.path.insert(0, ROOT)
+    import p1_amd
+
+    blob = p1_amd.codeobj_bytes()
+    assert blob[:4] == b"\x7fELF" and blob == embedded_code_object()
+    assert p1_amd.codeobj_sha256() == hashlib.sha256(blob).hexdigest()
+    hsaco = os.path.join(ROOT, "build", "p1hip_kernels.hsaco")
+    if os.path.exists(hsaco):
+        assert open(hsaco, "rb").read() == blob

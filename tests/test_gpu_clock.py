@@ -1,0 +1,46 @@
+"""The shader-clock probe bench.py brackets its timed steps with
+(tools/clock_probe.hip, bench.ClockProbe).
+
+Two stamps around a 2^34-nonce scan (about a third of a second of k_scan on
+every CU) must pair up on all 8 XCDs of cuda:0, give a clock inside the
+MI355X's range, and span the wall time of the scan they bracket.  The
+probe is measurement only: the scan's result is still checked against its
+pinned answer, and the code object hash bench.py reports is the embedded
+one."""
+import hashlib
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_clock_probe_brackets_a_scan(gpu, large):
+    import bench
+
+    probe = bench.ClockProbe([0])
+    assert probe.lib is not None, probe.error
+    msg = b"cmu440-p1-" * 12
+    want = large[(msg, 0, (1 << 34) - 1)]
+    assert gpu.scan(msg, 0, (1 << 34) - 1) == want  # warm: clocks up, tables built
+    before = probe.stamp()
+    t0 = time.perf_counter()
+    got = gpu.scan(msg, 0, (1 << 34) - 1)
+    wall = time.perf_counter() - t0
+    after = probe.stamp()
+    assert got == want
+    assert before and after, probe.error
+    xccs = {int(s[3]) for s in before[0]}
+    assert len(xccs) == 8, xccs  # 64 workgroups reach every XCD
+    rec = probe.clock(before, after)
+    dev = rec["devices"]["0"]
+    print("clock", rec["effective_clock_GHz"], dev.get("min_GHz"), dev.get("max_GHz"), "wall", wall,
+          "interval", dev.get("interval_s"), "wall counter kHz", dev.get("wall_counter_kHz"))
+    assert 1.0 < rec["effective_clock_GHz"] < 2.6 and not rec.get("implausible")
+    assert dev["max_GHz"] / dev["min_GHz"] < 1.05  # the XCDs share the clock
+    assert wall * 0.9 < dev["interval_s"] < wall + 0.05
+
+
+def test_bench_reports_the_embedded_code_object(gpu):
+    blob = gpu.codeobj_bytes()
+    assert gpu.codeobj_sha256() == hashlib.sha256(blob).hexdigest() and blob[:4] == b"\x7fELF"

@@ -233,3 +233,62 @@ def test_early_buffer_is_bounded_in_bytes():
     finally:
         srv.kill()
         srv.wait()
+
+
+def test_early_bytes_are_capped_per_source_host():
+    """one peer opening several connections (one per source
+    port) may not hold more early bytes than one connection may (64 MB), so
+    it cannot fill the server-wide pool (256 MB) and starve everyone else's
+    out-of-order Data.  Two connections from 127.0.0.1 each send 1,500 x 30 KB
+    = 43 MB of early messages: each is under its own 64 MB cap, together
+    they are acked for at most 64 MB."""
+    subprocess.run(["make", "-s", "-C", ROOT, "p1_amd/p1server"], check=True)
+    srv = subprocess.Popen([os.path.join(ROOT, "p1_amd", "p1server"), "--epoch-millis", "2000", "--epoch-limit", "50",
+                            "lsp", "0"], stdout=subprocess.PIPE, text=True)
+    socks = []
+    try:
+        line = srv.stdout.readline()
+        assert line.startswith("Server listening on port"), line
+        addr = ("127.0.0.1", int(line.split()[-1]))
+        conns = []
+        for _ in range(2):
+            s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+            s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 22)
+            s.settimeout(2.0)
+            s.sendto(lsp_msg(0, 0, 0, 0, None), addr)
+            conns.append(json.loads(s.recv(65536))["ConnID"])
+            s.settimeout(0.02)
+            socks.append(s)
+        assert conns[0] != conns[1]
+        p64 = b64(os.urandom(30000))
+        acked = [set(), set()]
+
+        def drain(k, deadline):
+            while time.monotonic() < deadline:
+                try:
+                    m = json.loads(socks[k].recv(65536))
+                except socket.timeout:
+                    return
+                except ValueError:
+                    continue
+                if m.get("Type") == 2 and m.get("SeqNum", 0) >= 2:
+                    acked[k].add(m["SeqNum"])
+
+        for seq in range(2, 1502):  # seq 1 never sent: everything is early
+            for k in (0, 1):
+                socks[k].sendto(lsp_msg(1, conns[k], seq, 30000, p64), addr)
+            if seq % 2 == 0:
+                drain(0, time.monotonic() + 0.02)
+                drain(1, time.monotonic() + 0.02)
+        drain(0, time.monotonic() + 0.5)
+        drain(1, time.monotonic() + 0.5)
+        held = [len(a) * 30000 / 2**20 for a in acked]
+        print("held MB per connection", [round(h, 1) for h in held])
+        assert srv.poll() is None
+        assert sum(held) <= 64.0 + 0.1, held
+        assert sum(held) > 40.0, held  # the host did get its share
+    finally:
+        for s in socks:
+            s.close()
+        srv.kill()
+        srv.wait()

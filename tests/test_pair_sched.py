@@ -1,9 +1,15 @@
 """tools/pair_sched.py: the post-RA reordering of loop segments for dual
 issue keeps every register dependency and never moves an instruction across
 a barrier.  CPU only."""
+import json
 import os
 import random
+import re
+import subprocess
 import sys
+import tempfile
+
+import pytest
 
 from conftest import ROOT
 
@@ -61,30 +67,122 @@ def _interpret(seg, order):
     return state
 
 
-def test_schedule_keeps_semantics_on_random_segments():
-    rng = random.Random(440)
-    for mode in (0, 2, 3):
-        for _ in range(30):
-            seg = _random_segment(rng)
-            order = pair_sched.schedule(seg, isa_post.issue_class, mode)
-            assert sorted(order) == list(range(len(seg)))
-            assert _interpret(seg, order) == _interpret(seg, range(len(seg)))
+# (run, amax, bmax): the uncapped modes and the run caps the build ships
+# (Makefile ISAPOST: --pair-sched=0 --sched-amax=5 --sched-bmax=4) and its
+# A/B neighbours
+SCHED_MODES = [(0, 0, 0), (2, 0, 0), (3, 0, 0), (0, 5, 4), (0, 5, 0), (0, 0, 4), (0, 3, 2), (0, 1, 1), (0, 8, 8)]
 
 
-def test_sticky_schedule_cuts_half_to_full_rate_transitions():
+@pytest.mark.parametrize("run,amax,bmax", SCHED_MODES)
+def test_schedule_keeps_semantics_on_random_segments(run, amax, bmax):
+    rng = random.Random(440 + 17 * amax + bmax)
+    for _ in range(30):
+        seg = _random_segment(rng)
+        order = pair_sched.schedule(seg, isa_post.issue_class, run, amax, bmax)
+        assert sorted(order) == list(range(len(seg)))
+        assert _interpret(seg, order) == _interpret(seg, range(len(seg)))
+
+
+def _transitions(seq):
+    v = [c for c in seq if c != "S"]
+    return sum(1 for x, y in zip(v, v[1:]) if x == "A" and y == "B")
+
+
+@pytest.mark.parametrize("amax,bmax", [(0, 0), (5, 4), (5, 0), (0, 4)])
+def test_sticky_schedule_cuts_half_to_full_rate_transitions(amax, bmax):
     rng = random.Random(441)
     before = after = 0
     for _ in range(20):
         seg = _random_segment(rng, n=200, nreg=40)
         cls = [isa_post.issue_class(s) for s in seg]
-        order = pair_sched.schedule(seg, isa_post.issue_class, 0)
-
-        def transitions(seq):
-            v = [c for c in seq if c != "S"]
-            return sum(1 for x, y in zip(v, v[1:]) if x == "A" and y == "B")
-        before += transitions(cls)
-        after += transitions([cls[i] for i in order])
+        order = pair_sched.schedule(seg, isa_post.issue_class, 0, amax, bmax)
+        before += _transitions(cls)
+        after += _transitions([cls[i] for i in order])
     assert after < before * 0.8, (before, after)
+
+
+def test_capped_runs_respect_their_caps_when_the_other_class_is_ready():
+    """amax / bmax: a run of one class is cut at the cap whenever an op of
+    the other class is ready -- on independent ops (always ready) the runs
+    are exactly the caps (a segment opens with the full-rate class)."""
+    seg = [f"v_alignbit_b32 v{i}, v{i}, v{i}, 7" for i in range(20)] + \
+          [f"v_add_u32_e64 v{100 + i}, v{100 + i}, v{100 + i}" for i in range(20)]
+    order = pair_sched.schedule(seg, isa_post.issue_class, 0, 5, 4)
+    cls = "".join(isa_post.issue_class(seg[i]) for i in order)
+    runs = [len(m.group(0)) for m in re.finditer(r"A+|B+", cls)]
+    assert max(len(r) for r in re.findall(r"A+", cls)) <= 5 and max(len(r) for r in re.findall(r"B+", cls)) <= 4
+    assert cls[0] == "B" and runs[:6] == [4, 5, 4, 5, 4, 5], cls  # full-rate first, then alternate at the caps
+
+
+def _region(body):
+    return [".LBB0_1:"] + ["\t" + s for s in body] + ["\ts_cbranch_scc0 .LBB0_1"]
+
+
+def test_hazard_check_trips_on_a_shortened_dpp_distance():
+    """the reorder may not move a VGPR write closer
+    than HAZARD_WINDOW wait states to a DPP read right after the segment.
+    Original order: v1 written first, then five independent ops; a schedule
+    that emits the half-rate write last brings it next to the DPP op."""
+    seg = ["v_alignbit_b32 v1, v1, v1, 7"] + [f"v_add_u32_e64 v{10 + i}, v{20 + i}, v{30 + i}" for i in range(5)]
+    dpp = "v_add_u32_dpp v2, v1, v3 row_ror:4 row_mask:0xf bank_mask:0xf"
+    order = [1, 2, 3, 4, 5, 0]
+    with pytest.raises(pair_sched.HazardError, match="v1"):
+        pair_sched.check_hazards(seg, order, [dpp], [])
+    pair_sched.check_hazards(seg, list(range(6)), [dpp], [])       # original order: fine
+    pair_sched.check_hazards(seg, order, ["v_cmp_lt_u32_e32 vcc, v1, v2"], [])  # plain VALU consumer: no wait
+    # far enough away: the write still sits 6 wait states before the DPP op
+    pair_sched.check_hazards(seg, order, ["s_nop 5", dpp], [])
+    with pytest.raises(pair_sched.HazardError):
+        pair_sched.check_hazards(seg, order, ["s_nop 3", dpp], [])
+    # a VMEM read of the moved write and a readlane of it are checked alike
+    for consumer in ("global_store_dword v[4:5], v1, off", "v_readlane_b32 s4, v1, 3"):
+        with pytest.raises(pair_sched.HazardError):
+            pair_sched.check_hazards(seg, order, [consumer], [])
+
+
+def test_hazard_check_trips_on_a_read_moved_next_to_a_transcendental():
+    seg = [f"v_add_u32_e64 v{10 + i}, v{20 + i}, v{30 + i}" for i in range(5)] + ["v_xor_b32_e64 v9, v1, v2"]
+    order = [5, 0, 1, 2, 3, 4]
+    with pytest.raises(pair_sched.HazardError, match="v1"):
+        pair_sched.check_hazards(seg, order, [], ["v_exp_f32_e32 v1, v7"])
+    pair_sched.check_hazards(seg, order, [], ["v_add_u32_e64 v1, v7, v8"])  # plain producer
+
+
+def test_pass_fails_the_build_on_a_hazard():
+    """Through the pass itself: a segment whose schedule moves a half-rate
+    write to its end, right before a DPP read of it, fails."""
+    body = ["v_alignbit_b32 v1, v1, v1, 7"] + [f"v_add_u32_e64 v{10 + i}, v{20 + i}, v{30 + i}" for i in range(5)] + \
+           ["v_add_u32_e64 v40, v41, v42", "v_add_u32_dpp v2, v1, v3 row_ror:4 row_mask:0xf bank_mask:0xf"]
+    lines = _region(body)
+    stats = {"sched_segments": 0, "sched_moved": 0}
+    order = pair_sched.schedule(body[:7], isa_post.issue_class, 0, 0, 0)
+    assert order.index(0) == 6  # the full-rate run goes first: the write lands next to the DPP read
+    with pytest.raises(pair_sched.HazardError):
+        pair_sched.pass_pair_sched(lines, [(0, len(lines) - 1)], isa_post.is_instr, isa_post.issue_class, stats, 0)
+    # the same segment with the DPP read further away (a barrier and 5 wait states between) passes
+    far = _region(body[:7] + ["v_cmp_lt_u32_e32 vcc, v1, v2", "s_nop 4", body[7]])
+    pair_sched.pass_pair_sched(far, [(0, len(far) - 1)], isa_post.is_instr, isa_post.issue_class, stats, 0)
+    assert stats["sched_segments"] >= 1
+
+
+def test_shipped_post_pass_output_passes_the_hazard_check():
+    """The shipped post-pass (Makefile ISAPOST) run on the build's compiler
+    output reproduces build/p1hip_kernels.post.s byte for byte with the
+    check in force: every reordered segment passes."""
+    src = os.path.join(ROOT, "build", "p1hip_kernels.s")
+    post = os.path.join(ROOT, "build", "p1hip_kernels.post.s")
+    if not (os.path.exists(src) and os.path.exists(post)):
+        pytest.skip("build/p1hip_kernels.s not built")
+    mk = open(os.path.join(ROOT, "Makefile")).read()
+    opts = next(ln for ln in mk.split("\n") if ln.startswith("ISAPOST ?=")).split("=", 1)[1].split()
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "post.s")
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_post.py"), src, out] + opts,
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr[-2000:]
+        stats = json.loads(r.stderr.strip().split("\n")[-1])
+        assert stats["hazard_checked"] == stats["sched_segments"] > 0, stats
+        assert open(out).read() == open(post).read()
 
 
 def test_segments_stop_at_barriers():

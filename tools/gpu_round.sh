@@ -34,6 +34,10 @@ if [ "${RUN_STRESS:-0}" = 1 ]; then
   step stress 300 python "$ROOT/tools/stress.py" ${STRESS_S:-150} > "$OUT/${TAG}_stress.json" 2> "$OUT/${TAG}_stress.err"
   P1HIP_TEST_KNOBS=1 P1HIP_MIN_FAST_THREADS=1 P1HIP_SMALL_MAX_NONCES=0 step stress_k3 300 python "$ROOT/tools/stress.py" ${STRESS_S:-150} 441 > "$OUT/${TAG}_stress_k3.json" 2> "$OUT/${TAG}_stress_k3.err"
 fi
+if [ "${RUN_SHARD_BALANCE:-0}" = 1 ]; then
+  # the N-GPU plan_shards / equal splits of configs[3], each shard timed alone on GPU 0
+  step shard_balance 300 python "$ROOT/tools/shard_balance.py" > "$OUT/${TAG}_shard_balance.jsonl" 2> "$OUT/${TAG}_shard_balance.err"
+fi
 if [ "${RUN_TORCHRUN8:-0}" = 1 ]; then
   # the driver's N = 8 launch shape on one GPU: 8 ranks, gloo all-gather
   step torchrun8 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29513 "$ROOT/bench.py" --gpus 8 --steps 2 --warmup 1 --dist-backend gloo > "$OUT/${TAG}_torchrun8.json" 2> "$OUT/${TAG}_torchrun8.err"
@@ -75,25 +79,36 @@ if [ "${RUN_ASAN_TEARDOWN:-0}" = 1 ]; then
     step san_stress_normal_exit 240 "$ROOT/tools/san/capi_san_stress" ${SAN_STRESS_S:-20} > "$OUT/${TAG}_san_stress_normal_exit.out" 2>&1
 fi
 cd /tmp && export TMPDIR=/tmp
-# kernel-trace stats and PMC passes per config (every k_scan launch of the
-# profiled command is a workload launch: --no-small-request)
-for cfg in ${PROF_CONFIGS:-c2}; do
-  pargs="--steps 1 --warmup 0 --no-cpu --no-small-request --no-by-config --config $cfg"
+# kernel-trace stats and PMC passes of one profiled job (every k_scan launch
+# of the profiled command is a workload launch: --no-small-request).  Each
+# command's bench JSON line is kept beside its output: it names the code
+# object the command ran (library.codeobj_sha256), which
+# tools/summarize_prof.py writes into the summaries.
+prof_one() {  # prof_one <name> <bench job args...>
+  local name=$1; shift
   if [ "${SKIP_PROF:-0}" != 1 ]; then
     # the kernel trace of a bench run shaped like the timed one (warm-up
     # steps, then timed steps): summarize_prof --skip-launches 2 averages the
-    # same launches bench.py's HIP events time
-    step rocprof_stats_$cfg 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_${cfg}_prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps ${PROF_STEPS:-3} --warmup 2 --no-cpu --no-small-request --no-by-config --config $cfg > "$OUT/${TAG}_${cfg}_prof_bench.json"
+    # same launches bench.py's own HIP events time
+    step rocprof_stats_$name 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_${name}_prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps ${PROF_STEPS:-3} --warmup 2 --no-cpu --no-small-request --no-by-config "$@" > "$OUT/${TAG}_${name}_prof_bench.json"
   fi
   if [ "${SKIP_PMC:-0}" != 1 ]; then
-    i=0
+    local i=0 set
     for set in "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_INSTS_VALU_INT32 SQ_INSTS_SALU" \
                "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE" \
                "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_IFETCH" \
                "FETCH_SIZE" "WRITE_SIZE"; do
       i=$((i+1))
-      step pmc_${cfg}_$i 300 rocprofv3 --pmc $set --kernel-include-regex '^k_scan$' -d "$OUT/${TAG}_${cfg}_pmc$i" -o pmc --output-format csv -- python3 "$ROOT/bench.py" $pargs
+      step pmc_${name}_$i 300 rocprofv3 --pmc $set --kernel-include-regex '^k_scan$' -d "$OUT/${TAG}_${name}_pmc$i" -o pmc --output-format csv -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu --no-small-request --no-by-config "$@" > "$OUT/${TAG}_${name}_pmc${i}_bench.json"
     done
   fi
+}
+for cfg in ${PROF_CONFIGS:-c2}; do
+  prof_one "$cfg" --config "$cfg"
+done
+# one tail layout per spec "L,START[,N]" (bench.py --layout), named L<L>d<digits>
+for spec in ${PROF_LAYOUTS:-}; do
+  IFS=, read -r L START _ <<< "$spec"
+  prof_one "L${L}d${#START}" --layout "$spec"
 done
 echo "== done"

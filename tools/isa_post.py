@@ -7,21 +7,28 @@ usage: isa_post.py IN.s OUT.s [--no-e64] [--drop-asm-nops]
                                [--pair-sched=0 [--sched-amax=K] [--sched-bmax=K]] [--prio=PB,PA]
                                A/B only: [--ab-nop=N [--nop-where=ab|abb|ba] [--ab-nop-table=..]]
                                          [--ba-nop=N] [--split-add3=F]
-shipped (Makefile ISAPOST): --align-loops=3 --loop-offset=4 --pair-sched=0
-  --sched-amax=5 --sched-bmax=4 --prio=0,1 --loop-parity
+shipped: the Makefile's ISAPOST line is the one source of the shipped
+  options (round 5 end: --no-e64 --align-loops=3 --loop-offset=4
+  --pair-sched=0 --sched-amax=5 --sched-bmax=4 --prio=0,1; no --loop-parity).
+  Items 1, 2, 4 and 5 below are A/B options kept for the record: the VOP3
+  widening (1) and the parity rule (2) were retired in round 5 (DESIGN.md 4
+  "The parity rule is retired"); the scheduler (3) also checks that no
+  reorder shortens a wait-state distance LLVM relied on (tools/pair_sched.py
+  check_hazards: the build fails if one does).
 
 What it does and why (measurements: tools/valu_runs on MI355X,
 profiles/r01s_valu_runs.jsonl, profiles/r01v_valu_runs.jsonl, and the
 scan-kernel A/Bs in profiles/r01n_e64_ab.jsonl, profiles/r01r_loop_offset_sweep.jsonl):
 
-1. VOP2 -> VOP3 encoding of full-rate integer ops (v_add_u32_e32 ->
+1. (A/B, retired: --no-e64 ships) VOP2 -> VOP3 encoding of full-rate integer ops (v_add_u32_e32 ->
    v_add_u32_e64, likewise lshrrev/lshlrev/xor/and/or/sub).  Same operation,
    same result.  LLVM always shrinks to the 4-byte VOP2 form; in a stream
    mixed with half-rate VOP3 ops (v_alignbit_b32, v_add3_u32) every 4-byte
    instruction shifts the byte parity of the 8-byte ones that follow (2).
    Only register / inline-constant operands are converted (gfx950 VOP3 takes
    no literal).
-2. Byte parity of 8-byte instructions in hot loops.  A wave stream that mixes
+2. (the --loop-parity part is an A/B option, retired) Byte parity of 8-byte
+   instructions in hot loops.  A wave stream that mixes
    half-rate VOP3 (4.3 SIMD cycles per wave instruction alone) with full-rate
    VOP3 (2.7) issues at the additive rate only when the 8-byte instructions
    sit at addresses = 4 (mod 8); at 0 (mod 8) EVERY instruction of the mix

@@ -47,7 +47,7 @@ def main():
             mx, mean = max(times), sum(times) / len(times)
             print(json.dumps({"n": n, "split": name, "shards": shards, "kernel_ms": times,
                               "max_over_mean": mx / mean, "implied_GH_s": TOTAL / (mx * 1e-3) / 1e9,
-                              "result": list(min(keys))}), flush=True)
+                              "result": list(min(keys)), "codeobj_sha256": p1_amd.codeobj_sha256()}), flush=True)
 
 
 if __name__ == "__main__":

@@ -11,18 +11,91 @@ usage: python tools/summarize_prof.py <TAG> [nonces_per_launch] [--config cN --n
   launch of it a workload launch: bench.py --no-small-request), per-nonce
   figures come from counters summed over ALL its launches -- needed when a
   step is several launches (configs[3]: 2 per 2^38 scan).
+
+  Every summary names the code object it measured:
+  `codeobj_sha256` in the PMC summary and a Codeobj_SHA256 column in the
+  workload CSV, read from the JSON lines the profiled bench commands printed
+  (gpurun_out/<TAG>_prof_bench.json, <TAG>_pmc*_bench.json: bench.py's
+  library.codeobj_sha256).  The commands must agree; bench.py cites only
+  summaries whose hash equals the code object it runs.
+
+  python tools/summarize_prof.py --retag TAG --codeobj-sha256 H --basis TEXT
+  adds the hash to an already committed TAG's summaries (profiles taken
+  before the hash was recorded), with the basis for the attribution.
 """
 import csv
 import glob
 import json
 import os
 import shutil
-import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def workload_stats(trace, out, skip=0):
+def codeobj_of(src, tag, explicit=None):
+    """sha256 of the code object the profiled commands of `tag` ran: every
+    bench JSON line they printed must name the same one (and match
+    `explicit` when given).  Raises SystemExit otherwise."""
+    seen = {}
+    for f in sorted(glob.glob(os.path.join(src, f"{tag}_prof_bench.json")) +
+                    glob.glob(os.path.join(src, f"{tag}_pmc*_bench.json"))):
+        for ln in open(f):
+            if ln.startswith("{"):
+                h = json.loads(ln).get("library", {}).get("codeobj_sha256")
+                if h:
+                    seen[os.path.basename(f)] = h
+    got = set(seen.values())
+    if explicit:
+        if got - {explicit}:
+            raise SystemExit(f"summarize_prof: --codeobj-sha256 {explicit} but the profiled commands ran {seen}")
+        return explicit, "given" if not seen else sorted(seen)
+    if len(got) != 1:
+        raise SystemExit(f"summarize_prof: need exactly one code object across the profiled commands, got {seen} "
+                         f"(pass --codeobj-sha256 for output without bench lines)")
+    return got.pop(), sorted(seen)
+
+
+def retag(tag, sha, basis):
+    """Add the code object hash to an already committed TAG's summaries."""
+    dst = os.path.join(ROOT, "profiles")
+    done = []
+    p = os.path.join(dst, f"{tag}_pmc_summary.json")
+    if os.path.exists(p):
+        d = json.load(open(p))
+        d["codeobj_sha256"], d["codeobj_source"] = sha, {"retagged": basis}
+        with open(p, "w") as f:
+            json.dump(d, f, indent=1)
+        done.append(p)
+    p = os.path.join(dst, f"{tag}_kernel_stats_workload.csv")
+    if os.path.exists(p):
+        rows = list(csv.DictReader(open(p)))
+        def num(v):
+            for t in (int, float):
+                try:
+                    return t(v)
+                except ValueError:
+                    pass
+            return v
+        write_stats_rows(p, [dict({k: num(v) for k, v in r.items()}, Codeobj_SHA256=sha) for r in rows])
+        done.append(p)
+    if not done:
+        raise SystemExit(f"summarize_prof: nothing committed under profiles/ for {tag}")
+    return done
+
+
+STATS_COLS = ["Name", "Calls", "TotalDurationNs", "AverageNs", "MinNs", "MaxNs", "StdDev", "Grid_Size_X", "Source",
+              "Codeobj_SHA256"]
+
+
+def write_stats_rows(path, rows):
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=STATS_COLS, quoting=csv.QUOTE_NONNUMERIC, extrasaction="ignore")
+        w.writeheader()
+        for r in rows:
+            w.writerow({k: r.get(k, "") for k in STATS_COLS})
+
+
+def workload_stats(trace, out, skip=0, codeobj=""):
     """rocprofv3 --kernel-trace rows of the workload's k_scan launches only
     (largest grid; bench.py's configs[0]-sized latency probe launches small
     grids of the same kernel), in the --stats CSV layout.  With skip > 0 a
@@ -35,15 +108,16 @@ def workload_stats(trace, out, skip=0):
     g = max(int(r["Grid_Size_X"]) for r in rows)
     rows = sorted((r for r in rows if int(r["Grid_Size_X"]) == g), key=lambda r: int(r["Start_Timestamp"]))
     d_all = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
-    with open(out, "w") as f:
-        f.write('"Name","Calls","TotalDurationNs","AverageNs","MinNs","MaxNs","StdDev","Grid_Size_X","Source"\n')
-        for name, d in (("k_scan", d_all), (f"k_scan (launches after the first {skip}: timed steps)", d_all[skip:])):
-            if not d or (name != "k_scan" and skip == 0):
-                continue
-            mean = sum(d) / len(d)
-            sd = (sum((x - mean) ** 2 for x in d) / len(d)) ** 0.5
-            f.write(f'"{name}",{len(d)},{sum(d)},{mean:.1f},{min(d)},{max(d)},{sd:.1f},{g},'
-                    f'"{os.path.basename(trace)}"\n')
+    out_rows = []
+    for name, d in (("k_scan", d_all), (f"k_scan (launches after the first {skip}: timed steps)", d_all[skip:])):
+        if not d or (name != "k_scan" and skip == 0):
+            continue
+        mean = sum(d) / len(d)
+        sd = (sum((x - mean) ** 2 for x in d) / len(d)) ** 0.5
+        out_rows.append({"Name": name, "Calls": len(d), "TotalDurationNs": sum(d), "AverageNs": round(mean, 1),
+                         "MinNs": min(d), "MaxNs": max(d), "StdDev": round(sd, 1), "Grid_Size_X": g,
+                         "Source": os.path.basename(trace), "Codeobj_SHA256": codeobj})
+    write_stats_rows(out, out_rows)
 
 
 # Measured issue cost (SIMD cycles per wave instruction at 4 waves/SIMD,
@@ -58,6 +132,9 @@ def main():
 
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
+    ap.add_argument("--codeobj-sha256", default=None)
+    ap.add_argument("--retag", action="store_true", help="add --codeobj-sha256 to TAG's committed summaries")
+    ap.add_argument("--basis", default=None, help="--retag: why the profile is of that code object")
     ap.add_argument("nonces_per_launch", nargs="?", type=float, default=2.0**32)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--nonces-total", type=float, default=None)
@@ -67,15 +144,21 @@ def main():
                     help="share of class-A (half-rate) instructions in the executed loop mix")
     a = ap.parse_args()
     tag, nonces = a.tag, a.nonces_per_launch
+    if a.retag:
+        if not (a.codeobj_sha256 and a.basis):
+            raise SystemExit("summarize_prof: --retag needs --codeobj-sha256 and --basis")
+        print("\n".join(retag(tag, a.codeobj_sha256, a.basis)))
+        return
     src = os.path.join(ROOT, "gpurun_out")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
+    codeobj, codeobj_src = codeobj_of(src, tag, a.codeobj_sha256)
     ks = os.path.join(src, f"{tag}_prof", "run_kernel_stats.csv")
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(dst, f"{tag}_kernel_stats.csv"))
     kt = os.path.join(src, f"{tag}_prof", "run_kernel_trace.csv")
     if os.path.exists(kt):
-        workload_stats(kt, os.path.join(dst, f"{tag}_kernel_stats_workload.csv"), a.skip_launches)
+        workload_stats(kt, os.path.join(dst, f"{tag}_kernel_stats_workload.csv"), a.skip_launches, codeobj)
     for f in glob.glob(os.path.join(src, f"{tag}_bench*.json")) + glob.glob(os.path.join(src, f"{tag}_valu_*.jsonl")):
         shutil.copy(f, os.path.join(dst, os.path.basename(f)))
     counters, durs, sums = {}, [], {}
@@ -100,7 +183,7 @@ def main():
     avg = {k: sum(v) / len(v) for k, v in counters.items()}
     dur = sum(durs) / len(durs)
     out = {"tag": tag, "config": a.config, "kernel": "k_scan", "avg_duration_s": dur,
-           "counters_per_launch": avg}
+           "counters_per_launch": avg, "codeobj_sha256": codeobj, "codeobj_source": codeobj_src}
     if a.nonces_total:
         out["nonces_total"] = a.nonces_total
         out["counters_total"] = sums
