@@ -577,6 +577,11 @@ def assemble_roofline(config, cfg, stats, steps, pmc=None, pmc_src=None, rocprof
             # average of the same command's timed launches, same code object
             roof["frac_rocprof"] = stats["scan_alg_ops"] / k_n / (avg_ns * 1e-9) / VALU_PEAK_OPS
             roof["rocprof_avg_launch_ms"] = avg_ns / 1e6
+            tr = (pmc or {}).get("trace_run") or {}
+            if tr.get("effective_clock_GHz"):
+                # the clock the traced command ran at (its own probe), so a
+                # gap between this run and the trace reads as clock or not
+                roof["rocprof_clock_GHz"] = tr["effective_clock_GHz"]
         else:
             stale.append("rocprof")
     roof["executed"] = None

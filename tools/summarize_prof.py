@@ -55,6 +55,23 @@ def codeobj_of(src, tag, explicit=None):
     return got.pop(), sorted(seen)
 
 
+def trace_run(src, tag):
+    """What the kernel-trace command's own bench line measured (its timed
+    steps, the shader clock its probe read): the trace's launch time and
+    the clock it ran at, side by side."""
+    f = os.path.join(src, f"{tag}_prof_bench.json")
+    if not os.path.exists(f):
+        return None
+    for ln in open(f):
+        if ln.startswith("{"):
+            d = json.loads(ln)
+            r = d.get("roofline", {})
+            return {"ms_per_step": d.get("ms_per_step"), "avg_launch_ms": r.get("avg_launch_ms"),
+                    "effective_clock_GHz": r.get("effective_clock_GHz"), "steps": d.get("steps"),
+                    "source": os.path.basename(f)}
+    return None
+
+
 def retag(tag, sha, basis):
     """Add the code object hash to an already committed TAG's summaries."""
     dst = os.path.join(ROOT, "profiles")
@@ -159,7 +176,8 @@ def main():
     kt = os.path.join(src, f"{tag}_prof", "run_kernel_trace.csv")
     if os.path.exists(kt):
         workload_stats(kt, os.path.join(dst, f"{tag}_kernel_stats_workload.csv"), a.skip_launches, codeobj)
-    for f in glob.glob(os.path.join(src, f"{tag}_bench*.json")) + glob.glob(os.path.join(src, f"{tag}_valu_*.jsonl")):
+    for f in (glob.glob(os.path.join(src, f"{tag}_bench*.json")) + glob.glob(os.path.join(src, f"{tag}_valu_*.jsonl"))
+              + glob.glob(os.path.join(src, f"{tag}_prof_bench.json"))):
         shutil.copy(f, os.path.join(dst, os.path.basename(f)))
     counters, durs, sums = {}, [], {}
     gmax_all = 0  # largest k_scan grid (threads) seen in the PMC passes
@@ -184,6 +202,9 @@ def main():
     dur = sum(durs) / len(durs)
     out = {"tag": tag, "config": a.config, "kernel": "k_scan", "avg_duration_s": dur,
            "counters_per_launch": avg, "codeobj_sha256": codeobj, "codeobj_source": codeobj_src}
+    tr = trace_run(src, tag)
+    if tr:
+        out["trace_run"] = tr
     if a.nonces_total:
         out["nonces_total"] = a.nonces_total
         out["counters_total"] = sums
