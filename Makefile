@@ -95,6 +95,10 @@ tools/wcal: tools/wcal.hip
 tools/libp1clock.so: tools/clock_probe.hip
 	$(HIPCC) -O2 -std=c++17 -fPIC -shared --offload-arch=$(ARCH) -Wall -o $@ tools/clock_probe.hip
 
+# measurement program: XCD dispatch order, per-XCD clock and finish time under load
+tools/xcd_probe: tools/xcd_probe.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ tools/xcd_probe.hip
+
 # measurement program: VALU issue cost vs operand VGPR banks
 tools/vbank: tools/vbank.hip
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -o $@ tools/vbank.hip

@@ -77,13 +77,14 @@ ALG_MIX = {"v_alignbit_b32": 576, "v_bitop3_b32": 352, "v_add3_u32": 240, "v_add
            "v_lshrrev_b32": 96}
 VALU_PEAK_PROFILE = "profiles/r01_valu_peak.jsonl"
 # Per-variant loop mix of the shipped kernel (tools/variant_report.py run
-# through the shipped post-pass in round 6: all 78 variants, VALU counts
-# identical to the r02d/r02k/r03f reports): A "half-rate" ops (v_alignbit_b32, v_add3_u32, ...)
+# through the shipped post-pass on the round-6 work-queue k_scan: all 78
+# variants; VALU counts identical to the r02d/r02k/r03f reports and to the
+# static-grid r06 report except 0,3 / 0,4 at 3 fewer): A "half-rate" ops (v_alignbit_b32, v_add3_u32, ...)
 # and B full-rate ops per nonce.  A SIMD issues VALU ops in 4-cycle slots; an
 # A op only as the first op of a slot, a B op also as the second (another
 # wave's), so a loop cannot issue in fewer than 4 x max(A, (A + B) / 2)
 # SIMD cycles per 64 nonces (DESIGN.md 4 "Dual issue", tools/gen_dual.py).
-VARIANT_PROFILES = ["profiles/r06_variant_report.jsonl"]
+VARIANT_PROFILES = ["profiles/r06d_variant_report.jsonl"]
 VARIANT_PROFILE = ", ".join(VARIANT_PROFILES)
 SLOT_CYCLES = 4.0  # SIMD cycles per VALU issue slot (gfx950; DESIGN.md 4 "Dual issue")
 

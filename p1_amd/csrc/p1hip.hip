@@ -150,6 +150,8 @@ struct Dev {
   hipFunction_t f_scan = nullptr, f_reduce = nullptr, f_pairs = nullptr, f_small = nullptr, f_kwtable = nullptr;
   Key* d_small_part = nullptr;  // kSmallMaxBlocks partials of k_scan_small
   uint32_t* d_ticket = nullptr; // k_scan_small's last-workgroup counter (0 between scans)
+  uint32_t* d_scan_ticket = nullptr;  // k_scan's work queue: [tiles handed out, workgroups done] (0 between launches)
+  uint32_t scan_grid = 0;       // k_scan workgroups the device holds at once (occupancy x CUs)
   bool small_used = false;      // this scan ran k_scan_small (result already in h_res[0])
   std::vector<hipEvent_t> evs;  // profiling event pool (pairs)
   // MODE 5 K+W tables on this device, least recently used first (built by
@@ -227,6 +229,7 @@ int dev_release(Dev& d) {
   if (d.d_gather) (void)hipFree(d.d_gather);
   if (d.d_small_part) (void)hipFree(d.d_small_part);
   if (d.d_ticket) (void)hipFree(d.d_ticket);
+  if (d.d_scan_ticket) (void)hipFree(d.d_scan_ticket);
   if (d.h_res) (void)hipHostFree(d.h_res);
   if (d.stream) (void)hipStreamDestroy(d.stream);
   if (d.mod) (void)hipModuleUnload(d.mod);
@@ -283,9 +286,22 @@ int init_devs(Runtime& R, const std::vector<int>& ords) {
     HIPCHK(hipModuleGetFunction(&d.f_kwtable, d.mod, "k_kwtable"));
     HIPCHK(hipMalloc(&d.d_small_part, sizeof(Key) * kSmallMaxBlocks));
     HIPCHK(hipMalloc(&d.d_ticket, sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&d.d_scan_ticket, 2 * sizeof(uint32_t)));
     // on the library's own stream: a null-stream call would give every
     // process a second hardware queue (8 miner processes share one GPU)
     HIPCHK(hipMemsetAsync(d.d_ticket, 0, sizeof(uint32_t), d.stream));
+    HIPCHK(hipMemsetAsync(d.d_scan_ticket, 0, 2 * sizeof(uint32_t), d.stream));
+    // k_scan's grid: every workgroup slot of the device once (the work queue
+    // hands the tiles out; p1hip_kernels.hip k_scan)
+    {
+      hipDeviceProp_t prop;
+      HIPCHK(hipGetDeviceProperties(&prop, d.ordinal));
+      int per_cu = 0;
+      HIPCHK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, d.f_scan, kBlock, 0));
+      if (per_cu < 1 || prop.multiProcessorCount < 1)
+        return fail(P1HIP_ERR_HIP, "k_scan occupancy: " + std::to_string(per_cu) + " blocks per CU");
+      d.scan_grid = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
+    }
     HIPCHK(hipStreamSynchronize(d.stream));
     HIPCHK(hipMalloc(&d.d_res, sizeof(Key)));
     HIPCHK(hipMalloc(&d.d_gather, sizeof(Key) * nd));
@@ -576,8 +592,14 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
       }
       HIPCHK(hipEventRecord(d.evs[nev], d.stream));
     }
+#ifdef P1_STATIC_GRID
     HIPCHK(launch(d.f_scan, B.blocks, kBlock, d.stream, (const Segment*)ds, (uint32_t)B.count,
                   (Key*)(d.d_part + part_off)));
+#else
+    // B.blocks tiles through a work queue on min(tiles, slots) workgroups
+    HIPCHK(launch(d.f_scan, std::min(B.blocks, d.scan_grid), kBlock, d.stream, (const Segment*)ds,
+                  (uint32_t)B.count, (Key*)(d.d_part + part_off), (uint32_t)B.blocks, d.d_scan_ticket));
+#endif
     if (profiling) {
       HIPCHK(hipEventRecord(d.evs[nev + 1], d.stream));
       nev += 2;

@@ -8,8 +8,9 @@
 // Replaces the miner's scan loop /root/reference/src/github.com/cmu440/bitcoin/
 // miner/miner.go:56-63:
 //   k_scan    -> one launch, one segment per planner piece (variant chosen per
-//                workgroup from the segment table: fast_thread<FV,NV,TRAIL>
-//                or generic_thread)
+//                tile from the segment table: fast_thread<FV,NV,TRAIL>
+//                or generic_thread); a work queue of workgroup-sized tiles
+//                over a grid the device holds at once
 //             -> per-thread best (hash, nonce) -> wave argmin with DPP
 //                (quad_perm, row_ror) + ds_swizzle + readlane -> LDS across
 //                the 4 waves -> one 16-byte partial per workgroup
@@ -90,14 +91,13 @@ __device__ __forceinline__ void block_min_store(Key k, Key* out) {
 #define P1_FAST_WAVES 4
 #endif
 
-// The scan kernel: every workgroup finds its segment (wave-uniform scalar
-// loop over the table), runs that segment's per-thread work and writes one
-// 16-byte partial.  All decades of a scan -- and their ragged edges -- share
-// one launch, so there is one grid drain per scan, filled by the short
-// segments that are placed last.
-extern "C" __global__ __launch_bounds__(kBlock, P1_FAST_WAVES) void k_scan(const Segment* __restrict__ segs,
-                                                                           uint32_t nseg, Key* __restrict__ part) {
-  const uint32_t b = blockIdx.x;
+// One tile of a scan: workgroup-sized work `b` finds its segment
+// (wave-uniform scalar loop over the table), runs that segment's per-thread
+// work and writes one 16-byte partial.  All decades of a scan -- and their
+// ragged edges -- share one launch, so there is one grid drain per scan,
+// filled by the short segments that are placed last.
+__device__ __forceinline__ void scan_tile(const Segment* __restrict__ segs, uint32_t nseg, Key* __restrict__ part,
+                                          uint32_t b) {
   uint32_t si = 0;
   while (si + 1 < nseg && segs[si + 1].block0 <= b) ++si;
   const Segment& S = segs[si];
@@ -122,6 +122,49 @@ extern "C" __global__ __launch_bounds__(kBlock, P1_FAST_WAVES) void k_scan(const
   }
   block_min_store<kBlock>(k, part + b);
 }
+
+#ifdef P1_STATIC_GRID
+// A/B (round 5 and before): one workgroup per tile, the grid is the tiles.
+extern "C" __global__ __launch_bounds__(kBlock, P1_FAST_WAVES) void k_scan(const Segment* __restrict__ segs,
+                                                                           uint32_t nseg, Key* __restrict__ part) {
+  scan_tile(segs, nseg, part, blockIdx.x);
+}
+#else
+// The scan kernel as a work queue over `ntiles` tiles (round 6).  The
+// hardware hands workgroup i to XCD i mod 8, and under this load the XCDs
+// do not run at one clock (tools/xcd_probe: the odd XCDs 1.5% below the
+// even ones, profiles/r06b_xcd.jsonl), so a grid of one workgroup per tile
+// waits for the slowest XCD's eighth of the work.  Here the grid is what
+// the device holds at once (p1hip.hip: occupancy x CUs, or ntiles if
+// fewer); each workgroup runs tile blockIdx.x, then takes the next tile
+// from an agent-scope counter until none is left, so a faster XCD simply
+// runs more tiles.  Every tile is still one workgroup's work with its own
+// partial at part[tile].  Every wave reads the same next tile from LDS, so
+// the whole workgroup leaves the loop together once the tiles run out.
+// ticket[0] counts tiles handed out, ticket[1] workgroups done; the last
+// workgroup to finish zeroes both for the stream's next launch.
+extern "C" __global__ __launch_bounds__(kBlock, P1_FAST_WAVES) void k_scan(const Segment* __restrict__ segs,
+                                                                           uint32_t nseg, Key* __restrict__ part,
+                                                                           uint32_t ntiles,
+                                                                           uint32_t* __restrict__ ticket) {
+  __shared__ uint32_t s_next;
+  uint32_t b = blockIdx.x;
+  for (;;) {
+    scan_tile(segs, nseg, part, b);
+    if (threadIdx.x == 0)
+      s_next = gridDim.x + __hip_atomic_fetch_add(&ticket[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    b = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_next);
+    if (b >= ntiles) break;
+  }
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(&ticket[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+    // every other workgroup has taken its last tile: nobody reads the counter again
+    __hip_atomic_store(&ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ticket[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+#endif
 
 extern "C" __global__ __launch_bounds__(kReduceThreads) void k_reduce(const Key* __restrict__ part, uint32_t n,
                                                                       Key* __restrict__ out) {

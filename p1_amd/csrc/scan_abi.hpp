@@ -59,7 +59,10 @@ struct SmallArgs {
 };
 
 // Kernel entry points (extern "C" names in the code object):
-//   k_scan(const Segment* segs, uint32_t nseg, Key* part)            grid: sum of segment blocks x kBlock
+//   k_scan(const Segment* segs, uint32_t nseg, Key* part, uint32_t ntiles, uint32_t* ticket)
+//                                     grid: min(ntiles, occupancy x CUs) x kBlock; tiles = sum of segment
+//                                     blocks, handed out through ticket[0..1] (0 between launches)
+//                                     (-DP1_STATIC_GRID: the first three arguments, grid = ntiles)
 //   k_reduce(const Key* part, uint32_t n, Key* out)                  grid: 1 x kReduceThreads
 //   k_pairs(const uint64_t* hs, const uint64_t* ns, uint64_t n, Key* part)  grid: ceil(n/kBlock) x kBlock
 //   k_scan_small(SmallArgs a)                                        grid: a.nblocks x kBlock

@@ -22,6 +22,7 @@ STREAM_FREE = {
     "hipDeviceGetPCIBusId", "hipEventCreate", "hipEventDestroy", "hipEventElapsedTime", "hipEventSynchronize", "hipFree",
     "hipGetDeviceCount", "hipGetDeviceProperties", "hipGetErrorString", "hipGetLastError", "hipHostFree",
     "hipHostMalloc", "hipMalloc", "hipModuleGetFunction", "hipModuleLoadData", "hipModuleUnload",
+    "hipModuleOccupancyMaxActiveBlocksPerMultiprocessor",  # k_scan's grid (a query of the function's resources)
     "hipSetDevice", "hipStreamCreateWithFlags", "hipStreamDestroy", "hipStreamSynchronize",
 }
 # calls that enqueue work: their stream argument (last) must be the device's

@@ -157,6 +157,9 @@ def main():
     ap.add_argument("--nonces-total", type=float, default=None)
     ap.add_argument("--skip-launches", type=int, default=0,
                     help="warm-up launches of the profiled command (second row of the workload stats)")
+    ap.add_argument("--tiles", type=int, default=None,
+                    help="k_scan tiles (16-B partials) per launch: since round 6 the grid is the device's "
+                         "workgroup slots and not the tiles (work queue), so the partial bytes need the count")
     ap.add_argument("--half-rate-share", type=float, default=None,
                     help="share of class-A (half-rate) instructions in the executed loop mix")
     a = ap.parse_args()
@@ -253,12 +256,14 @@ def main():
             c = json.load(open(cal[-1]))
             factor = c["k_part16"]["counted_over_actual"]
             out["write_bytes_per_launch_calibrated"] = out["write_bytes_per_launch"] / factor
-            out["partials_bytes_per_launch"] = gmax_all / 256 * 16
+            tiles = a.tiles if a.tiles else gmax_all / 256  # static grid (round 5 and before): workgroups = tiles
+            out["partials_bytes_per_launch"] = tiles * 16
+            out["tiles_per_launch"] = tiles
             out["traffic_note"] = (f"raw FETCH_SIZE+WRITE_SIZE per k_scan launch; WRITE_SIZE counts k_scan's "
                                    f"16-B-per-workgroup partial stores {factor:.2f}x "
                                    f"({os.path.relpath(cal[-1], ROOT)}), so the calibrated write bytes are "
                                    f"write_bytes_per_launch_calibrated against partials_bytes_per_launch "
-                                   f"(16 B x workgroups); FETCH is kernel arguments and segment tables")
+                                   f"(16 B x tiles); FETCH is kernel arguments and segment tables")
     with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
