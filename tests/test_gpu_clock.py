@@ -36,8 +36,12 @@ def test_clock_probe_brackets_a_scan(gpu, large):
     dev = rec["devices"]["0"]
     print("clock", rec["effective_clock_GHz"], dev.get("min_GHz"), dev.get("max_GHz"), "wall", wall,
           "interval", dev.get("interval_s"), "wall counter kHz", dev.get("wall_counter_kHz"))
-    assert 1.0 < rec["effective_clock_GHz"] < 2.6 and not rec.get("implausible")
-    assert dev["max_GHz"] / dev["min_GHz"] < 1.05  # the XCDs share the clock
+    assert 1.5 < rec["effective_clock_GHz"] < 2.6 and not rec.get("implausible")
+    # per XCD only plausible, not equal: the XCDs run at clocks of their own
+    # (profiles/r06b_xcd.jsonl), and over a quarter second the idle edges of
+    # the interval weigh in (r06a: 2.23-2.53, r06d: 1.91-2.66 GHz; over
+    # bench.py's ~100 s timed region 2.27-2.35)
+    assert 1.0 < dev["min_GHz"] and dev["max_GHz"] < 3.0 and len(dev["per_xcc_GHz"]) == 8
     assert wall * 0.9 < dev["interval_s"] < wall + 0.05
 
 
