@@ -102,7 +102,7 @@ constexpr uint32_t kMaxLaunchBlocks = 1u << 22;
 const char* const kTestKnobs[] = {
     "P1HIP_SMALL_MAX_NONCES", "P1HIP_MAX_LAUNCH_BLOCKS", "P1HIP_MAX_SCAN_SPAN", "P1HIP_KWTAB_MAX_BYTES",
     "P1HIP_NO_RCCL",          "P1HIP_FORCE_RCCL",        "P1HIP_MIN_FAST_THREADS", "P1HIP_TEST_FAIL_DEVICE",
-    "P1HIP_NO_TABLE",         "P1HIP_NO_SPLIT",
+    "P1HIP_NO_TABLE",         "P1HIP_NO_SPLIT",          "P1HIP_SCAN_GRID",
 };
 
 bool test_knobs_on() {
@@ -195,6 +195,8 @@ struct Runtime {
   //                           and a second kernel path to cross-check MODE 5)
   //   P1HIP_NO_SPLIT          straddling lo digits use mode 2 instead of the
   //                           split modes (A/B builds with -DP1_NV2_PLAIN)
+  //   P1HIP_SCAN_GRID         k_scan's grid (read per scan, scan_grid_for;
+  //                           large = one tile per workgroup, no queue)
   uint64_t min_fast_threads = kMinFastThreads;
   bool split = true;
   bool tabulate = true;
@@ -469,6 +471,17 @@ int kwtable_for(Dev& d, const Launch& L, uint64_t* dptr) {
   return P1HIP_OK;
 }
 
+// P1HIP_SCAN_GRID (tests / A/B only, read per scan): k_scan's grid instead of
+// the device's workgroup slots; at or above a launch's tile count every
+// workgroup runs one tile and the queue hands out none (the round-5
+// dispatch, on the same code object).
+uint32_t scan_grid_for(const Dev& d, uint32_t tiles) {
+  const char* v = test_knob("P1HIP_SCAN_GRID");
+  const uint64_t g = v ? strtoull(v, nullptr, 10) : 0;
+  const uint32_t slots = g > 0 ? (uint32_t)std::min<uint64_t>(g, kMaxLaunchBlocks) : d.scan_grid;
+  return std::min(tiles, slots);
+}
+
 // Run one device's share [lo, hi] (lo <= hi) and leave its Key in d.d_res.
 int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, bool profiling,
               uint64_t min_fast_threads, bool split, bool tabulate) {
@@ -597,7 +610,7 @@ int run_range(Dev& d, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, 
                   (Key*)(d.d_part + part_off)));
 #else
     // B.blocks tiles through a work queue on min(tiles, slots) workgroups
-    HIPCHK(launch(d.f_scan, std::min(B.blocks, d.scan_grid), kBlock, d.stream, (const Segment*)ds,
+    HIPCHK(launch(d.f_scan, scan_grid_for(d, B.blocks), kBlock, d.stream, (const Segment*)ds,
                   (uint32_t)B.count, (Key*)(d.d_part + part_off), (uint32_t)B.blocks, d.d_scan_ticket));
 #endif
     if (profiling) {

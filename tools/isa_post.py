@@ -4,7 +4,8 @@ Makefile: build/p1hip_kernels.s -> build/p1hip_kernels.post.s).
 
 usage: isa_post.py IN.s OUT.s [--no-e64] [--drop-asm-nops]
                                [--align-loops=P --loop-offset=B] [--loop-parity]
-                               [--pair-sched=0 [--sched-amax=K] [--sched-bmax=K]] [--prio=PB,PA]
+                               [--pair-sched=0 [--sched-amax=K] [--sched-bmax=K] [--strict-hazards]]
+                               [--prio=PB,PA]
                                A/B only: [--ab-nop=N [--nop-where=ab|abb|ba] [--ab-nop-table=..]]
                                          [--ba-nop=N] [--split-add3=F]
 shipped: the Makefile's ISAPOST line is the one source of the shipped
@@ -88,6 +89,10 @@ SAFE_NEXT = re.compile(r"^(v_add3_u32|v_add_u32_e(32|64)|v_alignbit_b32|v_lshrre
 REG = re.compile(r"^(v\d+|s\d+|vcc_lo|vcc_hi|vcc|exec_lo|exec_hi|m0|v\[\d+:\d+\]|s\[\d+:\d+\])$")
 RE_LABEL = re.compile(r"^(\.LBB\d+_\d+):")
 RE_BRANCH = re.compile(r"^s_cbranch_\w+\s+(\.LBB\d+_\d+)")
+# a loop's back edge: conditional, or an unconditional s_branch when LLVM
+# puts the exit test before the latch (the round-6 work-queue k_scan lays
+# out MODE 7's and the split modes' outer loops that way)
+RE_BACK = re.compile(r"^s_(?:cbranch_\w+|branch)\s+(\.LBB\d+_\d+)")
 LLVM_MC = os.environ.get("LLVM_MC", "/opt/rocm/lib/llvm/bin/llvm-mc")
 
 
@@ -232,11 +237,13 @@ def issue_class(ins):
 
 
 def loop_regions(lines):
+    """(header line, back-edge line) of every loop laid out header first: the
+    last branch to the header within 40,000 lines, conditional or not"""
     regions = []
     for h in loop_headers(lines):
         label = RE_LABEL.match(lines[h]).group(1)
-        for j in range(h + 1, min(len(lines), h + 40000)):
-            m = RE_BRANCH.match(lines[j].strip())
+        for j in range(min(len(lines), h + 40000) - 1, h, -1):
+            m = RE_BACK.match(lines[j].strip())
             if m and m.group(1) == label:
                 regions.append((h, j))
                 break
@@ -415,7 +422,8 @@ def main():
         stats.update(sched_segments=0, sched_moved=0)
         lines = pair_sched.pass_pair_sched(lines, loop_regions(lines), is_instr, issue_class, stats,
                                            3 if opt["--pair-sched"] is True else int(opt["--pair-sched"]),
-                                           int(opt.get("--sched-amax", 0)), int(opt.get("--sched-bmax", 0)))
+                                           int(opt.get("--sched-amax", 0)), int(opt.get("--sched-bmax", 0)),
+                                           strict="--strict-hazards" in opt)
     if "--ab-nop" in opt:
         table = None
         if "--ab-nop-table" in opt:  # N11,N12,N21,N22: (A-run 1|2+, B-run 1|2+)
