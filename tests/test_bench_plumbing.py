@@ -370,3 +370,23 @@ def test_bench_exits_5_on_a_bad_communicator():
     src = inspect.getsource(bench.main)
     assert "comm_info" in src and "sys.exit(5)" in src
     assert src.index("sys.exit(5)") < src.index("timed_steps(")
+
+
+def test_the_built_code_object_has_committed_profiles():
+    """The code object this tree builds has its rocprofv3 trace and PMC
+    summaries committed for every BASELINE config the N = 1 line times, so
+    the driver's line cites profiles of the kernels it runs (and its
+    scaling expectation uses this object's own one-GPU rate)."""
+    import p1_amd
+
+    try:
+        sha = p1_amd.codeobj_sha256()
+    except p1_amd.P1HipError:
+        pytest.skip("library not built")
+    for config in ("c4", "c2", "c3"):
+        pmc, src = bench.pmc_summary(config, sha)
+        avg, tsrc = bench.rocprof_row(config, sha)
+        assert pmc and avg, (config, sha)
+        assert pmc["trace_run"]["avg_launch_ms"] * 1e6 >= avg * 0.999, (config, src, tsrc)
+    e = bench.scaling_expectation("c4", 8, sha)
+    assert e["one_gpu_source"] == bench.rocprof_row("c4", sha)[1]
