@@ -263,7 +263,9 @@ def main():
                                    f"16-B-per-workgroup partial stores {factor:.2f}x "
                                    f"({os.path.relpath(cal[-1], ROOT)}), so the calibrated write bytes are "
                                    f"write_bytes_per_launch_calibrated against partials_bytes_per_launch "
-                                   f"(16 B x tiles); FETCH is kernel arguments and segment tables")
+                                   f"(16 B x tiles); FETCH is kernel arguments and segment tables; since round 6 "
+                                   f"the work queue adds one agent-scope atomic per tile (and one per workgroup "
+                                   f"at exit), which the write counters see as well")
     with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
