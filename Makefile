@@ -12,8 +12,10 @@ DEVHDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/fast_variants.in
 # (ISAPOST: LLVM's own encodings kept (--no-e64); loop labels aligned; every
 # loop body's straight-line segments reordered into runs of one issue class
 # (tools/pair_sched.py) with `s_setprio 1` / `s_setprio 0` before each
-# half-rate / full-rate run; DESIGN.md 4 "Dual issue") -> assembled + linked
-# code object, embedded in libp1hip.so.
+# half-rate / full-rate run; DESIGN.md 4 "Dual issue"; --strict-hazards: the
+# build fails if a reorder would shorten a wait-state distance LLVM relied
+# on, tools/pair_sched.py check_hazards) -> assembled + linked code object,
+# embedded in libp1hip.so.
 # -amdgpu-s-branch-bits=15: the post-pass inserts ~21.7k 4-byte s_setprio and
 # the loop-alignment padding AFTER the compiler has relaxed its branches, so
 # the compiler is told branches reach half their real range (+-2^14 of
@@ -23,7 +25,7 @@ DEVHDRS := $(CSRC)/sha256_dev.hpp $(CSRC)/scan_core.hpp $(CSRC)/fast_variants.in
 # branch that did not fit would fail the assembly ("branch size exceeds
 # simm16"), never build wrong code (tests/test_codeobj.py).
 DEVFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) --cuda-device-only -Wall -mllvm -amdgpu-s-branch-bits=15 $(DEVEXTRA)
-ISAPOST ?= --no-e64 --align-loops=3 --loop-offset=4 --pair-sched=0 --sched-amax=5 --sched-bmax=4 --prio=0,1
+ISAPOST ?= --no-e64 --align-loops=3 --loop-offset=4 --pair-sched=0 --sched-amax=5 --sched-bmax=4 --strict-hazards --prio=0,1
 BUILD := build
 
 all: p1_amd/libp1hip.so oracle tools/p1emu p1_amd/p1miner p1_amd/p1server p1_amd/p1client tools/lsp_scenarios \

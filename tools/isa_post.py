@@ -9,13 +9,15 @@ usage: isa_post.py IN.s OUT.s [--no-e64] [--drop-asm-nops]
                                A/B only: [--ab-nop=N [--nop-where=ab|abb|ba] [--ab-nop-table=..]]
                                          [--ba-nop=N] [--split-add3=F]
 shipped: the Makefile's ISAPOST line is the one source of the shipped
-  options (round 5 end: --no-e64 --align-loops=3 --loop-offset=4
-  --pair-sched=0 --sched-amax=5 --sched-bmax=4 --prio=0,1; no --loop-parity).
+  options (round 6: --no-e64 --align-loops=3 --loop-offset=4
+  --pair-sched=0 --sched-amax=5 --sched-bmax=4 --strict-hazards --prio=0,1;
+  no --loop-parity).
   Items 1, 2, 4 and 5 below are A/B options kept for the record: the VOP3
   widening (1) and the parity rule (2) were retired in round 5 (DESIGN.md 4
   "The parity rule is retired"); the scheduler (3) also checks that no
   reorder shortens a wait-state distance LLVM relied on (tools/pair_sched.py
-  check_hazards: the build fails if one does).
+  check_hazards: with --strict-hazards, shipped, the build fails if one
+  does; without it that segment keeps LLVM's order).
 
 What it does and why (measurements: tools/valu_runs on MI355X,
 profiles/r01s_valu_runs.jsonl, profiles/r01v_valu_runs.jsonl, and the
