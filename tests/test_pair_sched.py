@@ -212,3 +212,32 @@ def test_loop_regions_take_unconditional_back_edges():
              "\tv_add_u32_e32 v2, v2, v3", "\ts_cbranch_scc0 .LBB0_7", "\tv_add_u32_e32 v4, v4, v3",
              "\ts_branch .LBB0_7", ".LBB0_9:", "\ts_endpgm"]
     assert isa_post.loop_regions(lines) == [(0, 7)]
+
+
+def test_hoist_consts_moves_only_provably_invariant_moves():
+    """isa_post --hoist-consts (builds without MachineLICM): a constant move
+    leaves an innermost single-block loop only when it is the loop's one
+    write of its register, nothing before it in the body names that
+    register, and the header is entered only by its own back edge."""
+    lines = ["\ts_mov_b32 s9, 0", ".LBB0_4:                               ; =>This Inner Loop Header: Depth=1",
+             "\ts_mov_b32 s20, 0x428a2f98",       # hoistable
+             "\tv_add_u32_e32 v1, s20, v1",
+             "\ts_mov_b32 s21, 0x71374491",       # written twice: stays
+             "\tv_add_u32_e32 v2, s21, v2",
+             "\ts_mov_b32 s21, 0xb5c0fbcf",
+             "\tv_add_u32_e32 v3, s22, v3",       # s22 read before its move: stays
+             "\ts_mov_b32 s22, 0xe9b5dba5",
+             "\ts_add_i32 s9, s9, 1",
+             "\ts_cmp_lg_u32 s9, 10",
+             "\ts_cbranch_scc1 .LBB0_4",
+             "\ts_endpgm"]
+    stats = {}
+    out = isa_post.pass_hoist_consts(lines, stats)
+    assert stats["consts_hoisted"] == 1
+    assert out.index("\ts_mov_b32 s20, 0x428a2f98") < out.index(lines[1])
+    assert "\ts_mov_b32 s21, 0x71374491" in out[out.index(lines[1]):]
+    assert "\ts_mov_b32 s22, 0xe9b5dba5" in out[out.index(lines[1]):]
+    # a branch into the header from outside the loop: nothing moves
+    entered = lines[:1] + ["\ts_cbranch_scc0 .LBB0_4"] + lines[1:]
+    stats = {}
+    assert isa_post.pass_hoist_consts(entered, stats) == entered and not stats.get("consts_hoisted")

@@ -4,7 +4,7 @@ Makefile: build/p1hip_kernels.s -> build/p1hip_kernels.post.s).
 
 usage: isa_post.py IN.s OUT.s [--no-e64] [--drop-asm-nops]
                                [--align-loops=P --loop-offset=B] [--loop-parity]
-                               [--pair-sched=0 [--sched-amax=K] [--sched-bmax=K] [--strict-hazards]]
+                               [--hoist-consts] [--pair-sched=0 [--sched-amax=K] [--sched-bmax=K] [--strict-hazards]]
                                [--prio=PB,PA]
                                A/B only: [--ab-nop=N [--nop-where=ab|abb|ba] [--ab-nop-table=..]]
                                          [--ba-nop=N] [--split-add3=F]
@@ -336,6 +336,65 @@ def pass_split_add3(lines, frac, stats):
     return out
 
 
+RE_CONST_MOV = re.compile(r"^s_mov_b32\s+(s\d+),\s*(0x[0-9a-fA-F]+|-?\d+)\s*$")
+NO_DEF_OPS = re.compile(r"^(s_cmp|s_cbranch|s_branch|s_waitcnt|s_nop|s_setprio|s_barrier|s_endpgm|s_sleep|"
+                        r"global_store|buffer_store|flat_store|scratch_store|ds_write|s_store|s_dcache)")
+
+
+def pass_hoist_consts(lines, stats):
+    """A/B option --hoist-consts (for builds compiled without MachineLICM):
+    move `s_mov_b32 sN, <imm>` out of every innermost loop to just before
+    its header when that is provably the same program -- the loop is one
+    basic block entered only by falling into its header (every branch to
+    the header is the loop's own back edge), the move is the loop's only
+    write of sN and nothing in the body names sN before it.  The body runs
+    at least once, so sN holds the same constant after the loop too."""
+    import pair_sched
+
+    regions = loop_regions(lines)
+    inner = [r for r in regions if not any(o != r and r[0] < o[0] and o[1] < r[1] for o in regions)]
+    refs = {}
+    for k, ln in enumerate(lines):
+        m = re.search(r"\bs_(?:cbranch_\w+|branch)\s+(\.LBB\d+_\d+)", ln)
+        if m:
+            refs.setdefault(m.group(1), []).append(k)
+    move = {}  # line index -> header line index
+    for a, b in inner:
+        label = RE_LABEL.match(lines[a]).group(1)
+        if any(not (a < k <= b) for k in refs.get(label, [])):
+            continue
+        body = [k for k in range(a + 1, b + 1) if lines[k].strip() and not lines[k].strip().startswith(";")]
+        if any(RE_LABEL.match(lines[k].strip()) for k in body):
+            continue
+        seen = set()     # registers named so far in the body
+        defs = {}        # register -> number of writes in the body
+        for k in body:
+            t = lines[k].strip().split(";")[0].strip()
+            op, _, ops = t.partition(" ")
+            first = ops.split(",")[0] if ops else ""
+            if not NO_DEF_OPS.match(op):
+                for r in pair_sched.regs(first):
+                    defs[r] = defs.get(r, 0) + 1
+        for k in body:
+            t = lines[k].strip().split(";")[0].strip()
+            m = RE_CONST_MOV.match(t)
+            if m and m.group(1) not in seen and defs.get(m.group(1)) == 1:
+                move[k] = a
+            seen |= pair_sched.regs(t.partition(" ")[2])
+    out = []
+    hoist_at = {}
+    for k, h in move.items():
+        hoist_at.setdefault(h, []).append(lines[k])
+    for i, ln in enumerate(lines):
+        if i in move:
+            continue
+        if i in hoist_at:
+            out += hoist_at[i]
+            stats["consts_hoisted"] = stats.get("consts_hoisted", 0) + len(hoist_at[i])
+        out.append(ln)
+    return out
+
+
 def pass_prio(lines, prio_b, prio_a, stats):
     """A/B option --prio=PB,PA: `s_setprio PB` before the first full-rate op
     of every run and `s_setprio PA` before the first half-rate op of every
@@ -415,6 +474,8 @@ def main():
              "ab_nops": 0}
     lines = open(src).read().split("\n")
     lines = pass_encode(lines, "--no-e64" not in opt, "--drop-asm-nops" in opt, stats)
+    if "--hoist-consts" in opt:
+        lines = pass_hoist_consts(lines, stats)
     if "--align-loops" in opt:
         lines = pass_align(lines, int(opt["--align-loops"]), int(opt.get("--loop-offset", 0)), stats)
     if "--split-add3" in opt:
