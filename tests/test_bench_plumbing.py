@@ -390,3 +390,17 @@ def test_the_built_code_object_has_committed_profiles():
         assert pmc["trace_run"]["avg_launch_ms"] * 1e6 >= avg * 0.999, (config, src, tsrc)
     e = bench.scaling_expectation("c4", 8, sha)
     assert e["one_gpu_source"] == bench.rocprof_row("c4", sha)[1]
+
+
+def test_layout_config_profiles_one_tail_layout():
+    """--layout L,START[,N]: sweep.py's message, one decade, no pinned answer;
+    a range that crosses a decade (two kernel variants) is refused."""
+    c = bench.layout_config("43,1000000000000000")
+    assert c["msg"] == bytes((33 + (i * 7) % 90) for i in range(43)) and c["total"] == 1 << 32
+    assert c["layout"] == [43, 16] and c["variant"] == [14, 1, True] and c["b_tail"] == 2
+    assert (c["lo"], c["hi"]) == (10**15, 10**15 + (1 << 32) - 1)
+    assert bench.known_answer(c, 1) == (None, None)
+    assert bench.layout_config("8,1000000000,1000")["b_tail"] == 1
+    for bad in ("8", "8,999999999,2", "8,-1", "x,1"):
+        with pytest.raises((bench.UsageError, ValueError)):
+            bench.layout_config(bad)
